@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s (primary+shadow) of the per-pixel trace at 1920×1080 (BASELINE
+config 2: 16 spheres + 2 planes + 1 point light, Reinhard tonemap) on 1..N MI355X.
+
+Contract (driver):  python bench.py --gpus N --steps K --warmup W
+  * N=1 runs in-process; N>1 is launched by torch.distributed.run, one rank per GPU.
+  * A step = one pass of the hot path over one frame: Scene::RenderImage() of the C2 frame into
+    the float3 HDR framebuffer + the fused Reinhard tonemap to uint8 (RaytracingEngine.cpp:133),
+    everything resident in HBM (scene uploaded once, outputs stay on the device).
+  * N>1 is weak scaling: every rank renders its own frames (frames are independent, no
+    data-path collective).  `--mode tiled` instead splits ONE frame into row tiles across
+    ranks and assembles it on rank 0 with a gather over RCCL (torch.distributed "nccl").
+  * W untimed steps, then exactly K timed steps bracketed by barrier + synchronize on both
+    sides; the max over ranks is the time; rank 0 prints ONE JSON line.
+
+Extra fields: `roofline` (HBM-write bound of the dominant trace kernel from live per-launch HIP
+events; traffic from the committed PMC summary when present), `valu_fp64` (the algorithmic FP64
+flops / time against the FP64 vector peak), `cpu_baseline` (the unmodified reference renderer,
+oracle/_ref, timed on this host's cores; falls back to the C restatement "port").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (half the FP32 vector rate)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", help="c1..c5 (BASELINE configs), mirror, glass, mesh")
+    ap.add_argument("--mode", choices=["frames", "tiled"], default="frames")
+    ap.add_argument("--tonemap", default="reinhard_simple",
+                    help="fused LDR operator, or 'none' (HDR only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=6,
+                    help="reference frames timed for cpu_baseline (first one is warm-up)")
+    return ap.parse_args(argv)
+
+
+def alg_flops_per_ray(sc) -> int:
+    """F_ray = 25·Ns + 14·Np (+ 30·Nt for Möller–Trumbore)."""
+    return 25 * len(sc.spheres) + 14 * len(sc.planes) + 30 * len(sc.triangle_array())
+
+
+def load_traffic(config: str, mode: str):
+    """Per-launch HBM bytes of the trace kernel from the committed PMC summary, if any."""
+    path = os.path.join(HERE, "profiles", f"pmc_{config}_{mode}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as fh:
+        d = json.load(fh)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, HERE)
+
+
+def cpu_baseline(sc, rays_per_frame: int, frames: int):
+    """The reference CPU loop on this host: oracle/_ref/ref_harness (unmodified reference
+    Scene::RenderImage, OpenMP on all granted cores), median of frames-1 after one warm-up.
+    Falls back to the C restatement (kind "port") when the reference build is absent."""
+    from oracle import pyoracle as po
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    if po.ref_available():
+        _, ms, used = po.ref_render(sc, repeat=frames, threads=threads, want_image=False)
+        kind = "reference"
+    else:
+        ms = []
+        for _ in range(frames):
+            t0 = time.perf_counter()
+            po.render(sc, nthreads=threads)
+            ms.append((time.perf_counter() - t0) * 1e3)
+        used, kind = threads, "port"
+    timed = sorted(ms[1:] if len(ms) > 1 else ms)
+    med = timed[len(timed) // 2]
+    return {
+        "value": rays_per_frame / (med / 1e3) / 1e6,
+        "unit": "Mrays/s",
+        "cores": used,
+        "kind": kind,
+        "sample": f"{len(ms)} full {sc.camera.width}x{sc.camera.height} frames of config "
+                  f"{sc.name} (Scene::RenderImage only, first frame warm-up; median "
+                  f"{med:.1f} ms/frame)",
+        "ms_per_frame": med,
+    }
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    import torch
+    import torch.distributed as dist
+
+    from raytracingengine_amd import capi
+    from raytracingengine_amd.configs import make_config
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    tonemap = -1 if args.tonemap == "none" else capi.TONEMAPS.index(args.tonemap)
+    sc = make_config(args.config, aa=1)
+    W, H = sc.camera.width, sc.camera.height
+    ctx = capi.Context(local_rank)
+    stream = torch.cuda.Stream()
+    ctx.set_stream(stream.cuda_stream)
+    dscene = ctx.scene(sc)
+
+    if args.mode == "frames":
+        row0, row1 = 0, H
+    else:  # contiguous row tile per rank
+        row0, row1 = rank * H // world, (rank + 1) * H // world
+    rows = row1 - row0
+    hdr = torch.empty(rows * W * 3, dtype=torch.float32, device="cuda")
+    ldr = torch.empty(rows * W * 3, dtype=torch.uint8, device="cuda") if tonemap >= 0 else None
+    full = None
+    if args.mode == "tiled" and world > 1 and rank == 0:
+        full = [torch.empty(rows * W * 3, dtype=torch.float32, device="cuda") for _ in range(world)]
+
+    # ray counts of this rank's pixels (separate counting launch, not timed)
+    with torch.cuda.stream(stream):
+        ctx.reset_stats()
+        dscene.render_device(None, hdr.data_ptr(), None,
+                             capi.default_opts(tonemap=-1, row_begin=row0, row_end=row1,
+                                               flags=capi.RT_FLAG_COUNT_RAYS))
+        st = ctx.stats()
+    rays_rank = st.trace_rays + st.shadow_rays
+    ctx.reset_stats()
+
+    opts = capi.default_opts(tonemap=tonemap, row_begin=row0, row_end=row1)
+    timed_opts = capi.default_opts(tonemap=tonemap, row_begin=row0, row_end=row1,
+                                   flags=capi.RT_FLAG_TIME_KERNEL)
+
+    def step(o):
+        dscene.render_device(None, hdr.data_ptr(), ldr.data_ptr() if ldr is not None else None, o)
+        if args.mode == "tiled" and world > 1:
+            with torch.cuda.stream(stream):
+                dist.gather(hdr, full if rank == 0 else None, dst=0)
+
+    for _ in range(args.warmup):
+        step(opts)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed_opts)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kst = ctx.stats()
+    kernel_ms = kst.kernel_ms / max(1, kst.launches)
+
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+        r = torch.tensor([rays_rank], dtype=torch.float64, device="cuda")
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays_all = float(r[0])
+    else:
+        rays_all = float(rays_rank)
+
+    if args.mode == "frames":
+        total_rays = rays_all * args.steps          # every rank renders a full frame per step
+        frames = world * args.steps
+    else:
+        total_rays = rays_all * args.steps          # the ranks together render one frame
+        frames = args.steps
+    value = total_rays / elapsed / 1e6
+
+    if rank == 0:
+        px = rows * W
+        bytes_per_launch = px * (12 + (3 if tonemap >= 0 else 0))  # float3 HDR + uint8 LDR
+        achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9
+        traffic, traffic_src = load_traffic(args.config, args.mode)
+        flops = rays_rank * alg_flops_per_ray(sc)
+        line = {
+            "metric": "Mrays/sec (primary+shadow) at 1920x1080" if args.config == "c2"
+                      else f"Mrays/sec (primary+shadow), config {args.config}",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak" if args.mode == "frames" else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.config}: {W}x{H}, {len(sc.spheres)} spheres, "
+                            f"{len(sc.planes)} planes, {len(sc.lights)} point lights, AA=1, "
+                            f"float3 HDR + fused {args.tonemap} u8",
+                "global_batch": frames,
+                "resolution": [W, H],
+                "parallelism": (f"frames x{world}" if args.mode == "frames"
+                                else f"row-tiles x{world} + RCCL gather"),
+                "rays_per_frame": rays_all if args.mode == "tiled" else rays_rank,
+            },
+            "frames_per_sec": round(frames / elapsed, 3),
+            "kernel_ms_per_launch": round(kernel_ms, 6),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic,
+                "alg_bytes_per_launch": bytes_per_launch,
+                "traffic_source": traffic_src,
+            },
+            "valu_fp64": {
+                "achieved": round(flops / (kernel_ms / 1e3) / 1e12, 3),
+                "peak": FP64_VALU_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(flops / (kernel_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TFLOPS, 5),
+                "alg_flops_per_launch": flops,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(sc, rays_rank, args.cpu_frames)
+            except Exception as e:  # a reported baseline, never the product path
+                line["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(line), flush=True)
+
+    dscene.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,224 @@
+/*
+ * rt_capi.h — C-ABI of the MI355X (gfx950) renderer that replaces the CPU hot path of
+ * Sorax5/RaytracingEngine.  Plain C types only: pointers, sizes, PODs.  No exceptions cross
+ * this boundary; every entry point returns an rt_status and the message of the last failure
+ * on the calling thread is available from rt_last_error().
+ *
+ * Reference interface each entry point replaces (paths relative to /root/reference/RaytracingEngine):
+ *
+ *   rt_render / rt_render_device   std::vector<Vec3> Scene::RenderImage() const      Scene.h:311-328
+ *                                  (per pixel: GeneratePixelAt Scene.h:283-304 → TraceRay Scene.h:131-198
+ *                                   → IntersectClosest Scene.h:218-257, directLightning Scene.h:79-129,
+ *                                   computeTransmittance Scene.h:35-77, backgroundColor Scene.h:30-33)
+ *   rt_tonemap                     tonemap() RaytracingEngine.cpp:165-174 and the operators of
+ *                                  tonemapAll() RaytracingEngine.cpp:176-214, each followed by
+ *                                  toColor() RaytracingEngine.cpp:113-121
+ *   rt_scene_create                the scene state Scene::AddSphere/AddPlane/AddLight/AddTriangle/
+ *                                  AddModel accumulate (Scene.h:208-212)
+ *   rt_camera                      Camera (Math.h:85-122); antiAliasingAmount Math.h:94
+ *
+ * The C++20 drop-in headers under raytracingengine_amd/api/ (Math.h, Shape.h, Light.h, Scene.h,
+ * Image.h) are the reference-shaped API above this ABI; see INTEGRATION.md.
+ *
+ * Numerics: all geometry and shading is IEEE binary64 evaluated in the reference's operation
+ * order without FMA contraction, so images are bit-identical to the reference except where the
+ * reference calls libm pow/log (Blinn-Phong, Fresnel, Reinhard-Jodie), which may differ by an ulp.
+ */
+#ifndef RT_CAPI_H
+#define RT_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_CAPI_VERSION 1
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARG = 1, /* null pointer, zero size, inconsistent counts, bad row range   */
+    RT_ERR_HIP = 2,         /* a HIP runtime call failed (message names the call)           */
+    RT_ERR_OOM = 3,         /* device allocation failed                                     */
+    RT_ERR_UNSUPPORTED = 4, /* a request outside what this build implements                 */
+    RT_ERR_NO_DEVICE = 5    /* no gfx950 device at the requested ordinal                    */
+} rt_status;
+
+/* Material (Shape.h:13-19).  Defaults in the reference: shininess 128, specular 0,
+ * transparency 0, refractive_index 1. */
+typedef struct rt_material {
+    double color[3];
+    double shininess;
+    double specular;
+    double transparency;
+    double refractive_index;
+} rt_material;
+
+/* Sphere (Shape.h:59-133): centre = Transform.position, radius. */
+typedef struct rt_sphere {
+    double center[3];
+    double radius;
+    rt_material material;
+} rt_sphere;
+
+/* Plane (Shape.h:135-186).  `normal` is the normal as the Plane object stores it, i.e.
+ * already passed through Vec3::normalize() by the constructor (Shape.h:141-142). */
+typedef struct rt_plane {
+    double point[3];
+    double normal[3];
+    rt_material material;
+} rt_plane;
+
+/* Triangle (Shape.h:188-246): untranslated vertices plus Transform.position, which the
+ * reference adds to every vertex on each query (tv0/tv1/tv2, Shape.h:198-200).  A Model
+ * (Shape.h:248-307) is flattened into triangles that carry the model's material and
+ * translation.  Order in rt_scene_desc.triangles: the scene's standalone triangles in
+ * AddTriangle order, then every model's triangles in AddModel order and index order — the
+ * closest-hit order of Scene::IntersectClosest (Scene.h:243-254). */
+typedef struct rt_triangle {
+    double v0[3];
+    double v1[3];
+    double v2[3];
+    double translation[3];
+    rt_material material;
+} rt_triangle;
+
+/* Point light (Light.h:6-15). */
+typedef struct rt_light {
+    double position[3];
+    double color[3];
+    double intensity;
+} rt_light;
+
+typedef struct rt_scene_desc {
+    const rt_sphere* spheres;
+    int32_t n_spheres;
+    const rt_plane* planes;
+    int32_t n_planes;
+    const rt_triangle* triangles;
+    int32_t n_triangles;
+    const rt_light* lights;
+    int32_t n_lights;
+} rt_scene_desc;
+
+/* Camera (Math.h:85-122).  aa_samples = Camera::antiAliasingAmount (reference default 32).
+ * near/far are carried for API completeness; the trace does not read them (as in the
+ * reference). */
+typedef struct rt_camera {
+    double position[3];
+    double focal;
+    uint32_t width;
+    uint32_t height;
+    int32_t aa_samples;
+    int32_t _pad0;
+    double near_plane;
+    double far_plane;
+} rt_camera;
+
+/* Tonemap operators (RaytracingEngine.cpp:123-174), in tonemapAll()'s output order. */
+typedef enum rt_tonemap_op {
+    RT_TONEMAP_NONE = -1,                    /* no LDR output                               */
+    RT_TONEMAP_SIMPLE = 0,                   /* simple()                       :123-131     */
+    RT_TONEMAP_REINHARD = 1,                 /* reinhardSimple()               :133-135     */
+    RT_TONEMAP_REINHARD_EXTENDED = 2,        /* reinhardExtended(c, 5.0)       :137-141,193 */
+    RT_TONEMAP_REINHARD_EXTENDED_LUMINANCE = 3, /* reinhardExtendedLuminance(c, 5.0) :143-148,195 */
+    RT_TONEMAP_REINHARD_JODIE = 4,           /* reinhardJodie(c, 0.18)         :150-154     */
+    RT_TONEMAP_UNCHARTED2 = 5,               /* uncharted2()                   :156-163     */
+    RT_TONEMAP_ACES = 6,                     /* aces_approx() == tonemap()     :89-98,165   */
+    RT_TONEMAP_COUNT = 7
+} rt_tonemap_op;
+
+/* Soft-shadow extension (BASELINE config 5).  The reference has point lights only
+ * (Light.h); an area light is a build-defined extension with no reference semantics. */
+typedef struct rt_area_light {
+    double corner[3];    /* one corner of the parallelogram emitter                        */
+    double edge_u[3];    /* first edge vector                                              */
+    double edge_v[3];    /* second edge vector                                             */
+    double color[3];
+    double intensity;    /* total intensity, split evenly over the samples                 */
+    int32_t samples;     /* stratified samples per shading point (sqrt must be integral)   */
+    int32_t _pad0;
+} rt_area_light;
+
+typedef struct rt_render_opts {
+    int32_t max_recursion;   /* Scene::maxRecursion, reference value 10 (Scene.h:24)        */
+    int32_t tonemap;         /* rt_tonemap_op applied to the LDR output, if requested       */
+    double bias;             /* GeneratePixelAt's bias, reference value 1e-3 (Scene.h:291)  */
+    uint64_t seed;           /* key of the counter-based AA jitter RNG (samples 1..N-1)     */
+    uint32_t row_begin;      /* render rows [row_begin, row_end) only (row tiles for        */
+    uint32_t row_end;        /*  multi-GPU); row_end == 0 means the full image height       */
+    int32_t flags;           /* RT_FLAG_* bits                                              */
+    int32_t _pad0;
+} rt_render_opts;
+
+#define RT_FLAG_COUNT_RAYS 0x1   /* also run the ray-counting pass (fills rt_stats counts)   */
+#define RT_FLAG_TIME_KERNEL 0x2  /* bracket each render launch with HIP events              */
+
+/* Fills opts with the reference defaults: max_recursion 10, bias 1e-3, tonemap ACES,
+ * full image, seed 0x5EED, no flags. */
+void rt_render_opts_default(rt_render_opts* opts);
+
+typedef struct rt_stats {
+    uint64_t trace_rays;   /* TraceRay invocations that reach IntersectClosest              */
+    uint64_t shadow_rays;  /* computeTransmittance invocations                              */
+    double kernel_ms;      /* summed HIP-event time of render launches (RT_FLAG_TIME_KERNEL)*/
+    uint64_t launches;     /* render launches timed into kernel_ms                          */
+} rt_stats;
+
+typedef struct rt_context rt_context;
+typedef struct rt_scene rt_scene;
+
+/* Thread-local message of the most recent failure ("" if none). */
+const char* rt_last_error(void);
+
+/* Number of visible HIP devices (0 when none). */
+int rt_device_count(void);
+
+/* A context owns one HIP device, one stream and growable device buffers.  One context per
+ * host thread; calls on a context are not thread-safe. */
+rt_status rt_context_create(int device, rt_context** out);
+rt_status rt_context_destroy(rt_context* ctx);
+/* Make the context launch on an externally owned hipStream_t (NULL = its own stream). */
+rt_status rt_context_set_stream(rt_context* ctx, void* hip_stream);
+rt_status rt_context_synchronize(rt_context* ctx);
+
+/* Upload a scene to the context's device (done once; the render then reads it from HBM). */
+rt_status rt_scene_create(rt_context* ctx, const rt_scene_desc* desc, rt_scene** out);
+rt_status rt_scene_destroy(rt_scene* scene);
+/* Attach (or with NULL, detach) a build-defined area light to an uploaded scene. */
+rt_status rt_scene_set_area_light(rt_scene* scene, const rt_area_light* light);
+
+/* Synchronous host-buffer render: Scene::RenderImage().  Any of the three outputs may be
+ * NULL.  hdr64_out: rows*width*3 doubles, row-major, idx = (y-row_begin)*W + x, RGB (the
+ * reference's std::vector<Vec3> layout).  hdr32_out: the same as float.  ldr_out:
+ * rows*width*3 bytes of opts->tonemap followed by toColor().  stats may be NULL. */
+rt_status rt_render(rt_context* ctx, const rt_scene* scene, const rt_camera* cam,
+                    const rt_render_opts* opts, double* hdr64_out, float* hdr32_out,
+                    uint8_t* ldr_out, rt_stats* stats);
+
+/* Asynchronous render into DEVICE buffers on the context's stream (inputs and outputs stay
+ * resident in HBM).  Same layouts as rt_render; pointers are device pointers or NULL. */
+rt_status rt_render_device(rt_context* ctx, const rt_scene* scene, const rt_camera* cam,
+                           const rt_render_opts* opts, void* d_hdr64, void* d_hdr32,
+                           void* d_ldr);
+
+/* Ray counts (and, with RT_FLAG_TIME_KERNEL, accumulated kernel time) since the last reset. */
+rt_status rt_stats_read(rt_context* ctx, rt_stats* out);
+rt_status rt_stats_reset(rt_context* ctx);
+
+/* Device tonemap of host FP64 radiance: op in [0, RT_TONEMAP_COUNT) writes n*3 bytes;
+ * op == RT_TONEMAP_COUNT writes all seven operators, tonemapAll() order, 7*n*3 bytes. */
+rt_status rt_tonemap(rt_context* ctx, const double* hdr, size_t n_pixels, int op,
+                     uint8_t* ldr_out);
+
+/* Test hook: evaluates x/y, sqrt(x), pow(x,y), log(x) on the device for n inputs so the
+ * parity suite can pin device libm against the host's.  out: 4*n doubles. */
+rt_status rt_debug_f64_ops(rt_context* ctx, const double* x, const double* y, size_t n,
+                           double* out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* RT_CAPI_H */

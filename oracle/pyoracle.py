@@ -1,0 +1,172 @@
+"""ctypes front-end of the C oracle (oracle/liboracle.so) and of the compiled reference
+(oracle/_ref/ref_harness).  TEST INFRASTRUCTURE ONLY: imported by tests/, by
+``__graft_entry__.smoke()`` and by bench.py's cpu_baseline leg — never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+
+from raytracingengine_amd.scene import AREA_LIGHT_DTYPE, SceneData
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+REF_HARNESS = os.path.join(HERE, "_ref", "ref_harness")
+
+
+class _Scene(ctypes.Structure):
+    _fields_ = [
+        ("spheres", ctypes.c_void_p), ("n_spheres", ctypes.c_int32),
+        ("planes", ctypes.c_void_p), ("n_planes", ctypes.c_int32),
+        ("triangles", ctypes.c_void_p), ("n_triangles", ctypes.c_int32),
+        ("lights", ctypes.c_void_p), ("n_lights", ctypes.c_int32),
+    ]
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [
+        ("max_recursion", ctypes.c_int32), ("nthreads", ctypes.c_int32),
+        ("bias", ctypes.c_double), ("seed", ctypes.c_uint64),
+        ("row_begin", ctypes.c_uint32), ("row_end", ctypes.c_uint32),
+        ("area_light", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def build():
+    """Compile liboracle.so (and oracle/_ref where /root/reference exists) via oracle/Makefile."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, dp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)
+        L.oracle_render.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.oracle_render.restype = ctypes.c_int
+        L.oracle_tonemap.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, vp]
+        L.oracle_u01.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_u01.restype = ctypes.c_double
+        for n in ("oracle_sphere_intersect", "oracle_plane_intersect", "oracle_triangle_intersect"):
+            getattr(L, n).argtypes = [vp, vp, dp]
+            getattr(L, n).restype = ctypes.c_int
+        L.oracle_get_ray.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                     ctypes.c_uint64, ctypes.c_uint32, vp]
+        L.oracle_closest.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_int32)]
+        L.oracle_closest.restype = ctypes.c_int
+        L.oracle_transmittance.argtypes = [vp, vp, ctypes.c_double, ctypes.c_double]
+        L.oracle_transmittance.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+class OracleScene:
+    """Keeps the numpy buffers alive for as long as the C view of them is used."""
+
+    def __init__(self, sc: SceneData):
+        self.sc = sc
+        self.spheres = sc.sphere_array()
+        self.planes = sc.plane_array()
+        self.triangles = sc.triangle_array()
+        self.lights = sc.light_array()
+        self.camera = sc.camera.to_struct()
+        self.area = sc.area_light.to_struct() if sc.area_light is not None else None
+        self.c = _Scene(self.spheres.ctypes.data, len(self.spheres),
+                        self.planes.ctypes.data, len(self.planes),
+                        self.triangles.ctypes.data, len(self.triangles),
+                        self.lights.ctypes.data, len(self.lights))
+
+
+def render(sc: SceneData, max_recursion=10, bias=1e-3, seed=0x5EED, rows=None, nthreads=0,
+           use_area_light=True):
+    """Scene::RenderImage restated in C.  Returns (hdr[rows,W,3] float64, trace, shadow)."""
+    L = lib()
+    os_ = OracleScene(sc)
+    r0, r1 = (0, sc.camera.height) if rows is None else rows
+    out = np.empty((r1 - r0, sc.camera.width, 3), np.float64)
+    opts = _Opts(max_recursion, nthreads, bias, seed, r0, r1,
+                 os_.area.ctypes.data if (os_.area is not None and use_area_light) else None)
+    nt, ns = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = L.oracle_render(ctypes.addressof(os_.c), os_.camera.ctypes.data, ctypes.addressof(opts),
+                         out.ctypes.data, ctypes.addressof(nt), ctypes.addressof(ns))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render failed ({rc})")
+    return out, nt.value, ns.value
+
+
+def tonemap(hdr: np.ndarray, op: int) -> np.ndarray:
+    hdr = np.ascontiguousarray(hdr, dtype=np.float64).reshape(-1, 3)
+    out = np.empty(hdr.shape, np.uint8)
+    if lib().oracle_tonemap(hdr.ctypes.data, hdr.shape[0], op, out.ctypes.data) != 0:
+        raise ValueError(op)
+    return out
+
+
+def u01(seed, pixel, stream, index) -> float:
+    return lib().oracle_u01(seed, pixel, stream, index)
+
+
+def sphere_intersect(ray, center, radius):
+    s = np.zeros(1, np.dtype([("c", "<f8", (3,)), ("r", "<f8"), ("m", "<f8", (7,))]))
+    s["c"][0], s["r"][0] = center, radius
+    r = np.ascontiguousarray(ray, np.float64)
+    t = ctypes.c_double(0)
+    hit = lib().oracle_sphere_intersect(r.ctypes.data, s.ctypes.data, ctypes.byref(t))
+    return (t.value if hit else None)
+
+
+def get_ray(sc: SceneData, x, y, aa=False, seed=0, sample=0):
+    cam = sc.camera.to_struct()
+    out = np.empty(6, np.float64)
+    lib().oracle_get_ray(cam.ctypes.data, x, y, int(aa), seed, sample, out.ctypes.data)
+    return out
+
+
+def closest(sc: SceneData, ray):
+    os_ = OracleScene(sc)
+    r = np.ascontiguousarray(ray, np.float64)
+    out = np.zeros(7, np.float64)
+    idx = ctypes.c_int32(-1)
+    typ = lib().oracle_closest(ctypes.addressof(os_.c), r.ctypes.data, out.ctypes.data,
+                               ctypes.byref(idx))
+    return typ, idx.value, out
+
+
+# ------------------------------------------------------------------ compiled reference
+def ref_available() -> bool:
+    return os.path.exists(REF_HARNESS)
+
+
+def ref_render(sc: SceneData, repeat: int = 1, threads: int | None = None, want_image=True):
+    """Run the unmodified reference Scene::RenderImage on `sc`.  Returns (hdr or None, ms list,
+    threads).  AA>1 renders are non-deterministic in the reference (random_device seed)."""
+    if not ref_available():
+        raise FileNotFoundError(REF_HARNESS)
+    with tempfile.TemporaryDirectory() as td:
+        scene_path = os.path.join(td, "scene.txt")
+        out_path = os.path.join(td, "out.f64") if want_image else "-"
+        sc.write(scene_path)
+        env = dict(os.environ)
+        if threads is not None:
+            env["OMP_NUM_THREADS"] = str(threads)
+        res = subprocess.run([REF_HARNESS, "render", scene_path, out_path, str(repeat)],
+                             check=True, capture_output=True, text=True, env=env)
+        info = json.loads(res.stdout.strip().splitlines()[-1])
+        img = None
+        if want_image:
+            img = np.fromfile(out_path, np.float64).reshape(sc.camera.height, sc.camera.width, 3)
+        return img, info["ms"], info["threads"]
+
+
+def ref_run(mode: str, *args: str) -> None:
+    subprocess.run([REF_HARNESS, mode, *map(str, args)], check=True, capture_output=True)

@@ -1,0 +1,261 @@
+"""ctypes binding of ``include/rt_capi.h`` (the HIP library ``librtamd.so``).
+
+This is plumbing for the bench and the parity tests: every call goes straight to the C-ABI.
+There is no CPU fallback — if the library or a gfx950 device is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .scene import AREA_LIGHT_DTYPE, SceneData
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtamd.so")
+
+RT_OK, RT_ERR_INVALID_ARG, RT_ERR_HIP, RT_ERR_OOM, RT_ERR_UNSUPPORTED, RT_ERR_NO_DEVICE = range(6)
+STATUS_NAMES = {0: "RT_OK", 1: "RT_ERR_INVALID_ARG", 2: "RT_ERR_HIP", 3: "RT_ERR_OOM",
+                4: "RT_ERR_UNSUPPORTED", 5: "RT_ERR_NO_DEVICE"}
+
+TONEMAP_NONE = -1
+TONEMAPS = ["simple", "reinhard_simple", "reinhard_extended", "reinhard_extended_luminance",
+            "reinhard_jodie", "uncharted2", "aces"]
+TONEMAP_ALL = 7
+RT_FLAG_COUNT_RAYS = 0x1
+RT_FLAG_TIME_KERNEL = 0x2
+
+# Every symbol include/rt_capi.h declares (checked by tests/test_capi_symbols.py).
+EXPORTED = [
+    "rt_last_error", "rt_device_count", "rt_render_opts_default", "rt_context_create",
+    "rt_context_destroy", "rt_context_set_stream", "rt_context_synchronize", "rt_scene_create",
+    "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
+    "rt_stats_read", "rt_stats_reset", "rt_tonemap", "rt_debug_f64_ops",
+]
+
+
+class RtError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [
+        ("spheres", ctypes.c_void_p), ("n_spheres", ctypes.c_int32),
+        ("planes", ctypes.c_void_p), ("n_planes", ctypes.c_int32),
+        ("triangles", ctypes.c_void_p), ("n_triangles", ctypes.c_int32),
+        ("lights", ctypes.c_void_p), ("n_lights", ctypes.c_int32),
+    ]
+
+
+class RenderOpts(ctypes.Structure):
+    _fields_ = [
+        ("max_recursion", ctypes.c_int32), ("tonemap", ctypes.c_int32),
+        ("bias", ctypes.c_double), ("seed", ctypes.c_uint64),
+        ("row_begin", ctypes.c_uint32), ("row_end", ctypes.c_uint32),
+        ("flags", ctypes.c_int32), ("_pad0", ctypes.c_int32),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("trace_rays", ctypes.c_uint64), ("shadow_rays", ctypes.c_uint64),
+        ("kernel_ms", ctypes.c_double), ("launches", ctypes.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load librtamd.so; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7; loading it first
+        # makes librtamd.so's NEEDED entry bind to that copy instead of /opt/rocm's.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (hipcc --offload-arch=gfx950). The renderer has no CPU fallback.")
+    L = ctypes.CDLL(path)
+    vp, i32 = ctypes.c_void_p, ctypes.c_int
+    L.rt_last_error.restype = ctypes.c_char_p
+    L.rt_device_count.restype = i32
+    L.rt_render_opts_default.argtypes = [vp]
+    L.rt_render_opts_default.restype = None
+    for name, args in {
+        "rt_context_create": [i32, vp],
+        "rt_context_destroy": [vp],
+        "rt_context_set_stream": [vp, vp],
+        "rt_context_synchronize": [vp],
+        "rt_scene_create": [vp, vp, vp],
+        "rt_scene_destroy": [vp],
+        "rt_scene_set_area_light": [vp, vp],
+        "rt_render": [vp, vp, vp, vp, vp, vp, vp, vp],
+        "rt_render_device": [vp, vp, vp, vp, vp, vp, vp],
+        "rt_stats_read": [vp, vp],
+        "rt_stats_reset": [vp],
+        "rt_tonemap": [vp, vp, ctypes.c_size_t, i32, vp],
+        "rt_debug_f64_ops": [vp, vp, vp, ctypes.c_size_t, vp],
+    }.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = i32
+    _lib = L
+    return L
+
+
+def _check(status: int):
+    if status != RT_OK:
+        raise RtError(status, _lib.rt_last_error().decode(errors="replace"))
+
+
+def default_opts(**kw) -> RenderOpts:
+    o = RenderOpts()
+    load_library().rt_render_opts_default(ctypes.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def device_count() -> int:
+    return load_library().rt_device_count()
+
+
+class Context:
+    """One HIP device + stream (rt_context)."""
+
+    def __init__(self, device: int = 0):
+        L = load_library()
+        self._h = ctypes.c_void_p()
+        _check(L.rt_context_create(device, ctypes.byref(self._h)))
+        self.device = device
+
+    def close(self):
+        if self._h:
+            _lib.rt_context_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, stream_ptr: int | None):
+        _check(_lib.rt_context_set_stream(self._h, stream_ptr))
+
+    def synchronize(self):
+        _check(_lib.rt_context_synchronize(self._h))
+
+    def scene(self, sc: SceneData) -> "DeviceScene":
+        return DeviceScene(self, sc)
+
+    def stats(self) -> Stats:
+        s = Stats()
+        _check(_lib.rt_stats_read(self._h, ctypes.byref(s)))
+        return s
+
+    def reset_stats(self):
+        _check(_lib.rt_stats_reset(self._h))
+
+    def tonemap(self, hdr: np.ndarray, op: int) -> np.ndarray:
+        hdr = np.ascontiguousarray(hdr, np.float64).reshape(-1, 3)
+        planes = 7 if op == TONEMAP_ALL else 1
+        out = np.empty((planes, hdr.shape[0], 3), np.uint8)
+        _check(_lib.rt_tonemap(self._h, hdr.ctypes.data, hdr.shape[0], op, out.ctypes.data))
+        return out if planes > 1 else out[0]
+
+    def debug_f64_ops(self, x: np.ndarray, y: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, np.float64)
+        y = np.ascontiguousarray(y, np.float64)
+        out = np.empty((x.size, 4), np.float64)
+        _check(_lib.rt_debug_f64_ops(self._h, x.ctypes.data, y.ctypes.data, x.size,
+                                     out.ctypes.data))
+        return out
+
+
+class DeviceScene:
+    """A scene uploaded to HBM (rt_scene) plus the camera it is rendered with."""
+
+    def __init__(self, ctx: Context, sc: SceneData):
+        self.ctx = ctx
+        self.data = sc
+        self._arrays = (sc.sphere_array(), sc.plane_array(), sc.triangle_array(), sc.light_array())
+        sp, pl, tr, lt = self._arrays
+        desc = SceneDesc(sp.ctypes.data if len(sp) else None, len(sp),
+                         pl.ctypes.data if len(pl) else None, len(pl),
+                         tr.ctypes.data if len(tr) else None, len(tr),
+                         lt.ctypes.data if len(lt) else None, len(lt))
+        self._h = ctypes.c_void_p()
+        _check(_lib.rt_scene_create(ctx.handle, ctypes.byref(desc), ctypes.byref(self._h)))
+        self.camera = sc.camera.to_struct()
+        self._area = None
+        if sc.area_light is not None:
+            self._area = sc.area_light.to_struct()
+            _check(_lib.rt_scene_set_area_light(self._h, self._area.ctypes.data))
+
+    def close(self):
+        if self._h:
+            _lib.rt_scene_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def render(self, *, hdr64=True, hdr32=False, tonemap: int = TONEMAP_NONE, opts=None,
+               stats=False, **opt_kw):
+        """Synchronous render into host arrays (rt_render).  Returns dict of outputs."""
+        cam = self.data.camera
+        o = opts if opts is not None else default_opts(tonemap=tonemap, **opt_kw)
+        if opts is None:
+            o.tonemap = tonemap
+        r0 = o.row_begin
+        r1 = o.row_end or cam.height
+        rows = r1 - r0 if r1 > r0 else 0
+        out = {}
+        a64 = np.empty((rows, cam.width, 3), np.float64) if hdr64 else None
+        a32 = np.empty((rows, cam.width, 3), np.float32) if hdr32 else None
+        ldr = np.empty((rows, cam.width, 3), np.uint8) if tonemap != TONEMAP_NONE else None
+        st = Stats()
+        _check(_lib.rt_render(self.ctx.handle, self._h, self.camera.ctypes.data, ctypes.byref(o),
+                              a64.ctypes.data if a64 is not None else None,
+                              a32.ctypes.data if a32 is not None else None,
+                              ldr.ctypes.data if ldr is not None else None,
+                              ctypes.byref(st) if stats else None))
+        if a64 is not None:
+            out["hdr64"] = a64
+        if a32 is not None:
+            out["hdr32"] = a32
+        if ldr is not None:
+            out["ldr"] = ldr
+        if stats:
+            out["trace_rays"] = st.trace_rays
+            out["shadow_rays"] = st.shadow_rays
+        return out
+
+    def render_device(self, d_hdr64: int | None, d_hdr32: int | None, d_ldr: int | None,
+                      opts: RenderOpts):
+        """Asynchronous render into device pointers (rt_render_device)."""
+        _check(_lib.rt_render_device(self.ctx.handle, self._h, self.camera.ctypes.data,
+                                     ctypes.byref(opts), d_hdr64, d_hdr32, d_ldr))

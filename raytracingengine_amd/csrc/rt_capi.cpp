@@ -1,0 +1,613 @@
+// rt_capi.cpp — implementation of include/rt_capi.h on HIP (gfx950).
+//
+// The context owns a device, a stream and growable device staging buffers; a scene is one
+// HBM allocation of packed records (rt_internal.hpp).  No exception crosses the C boundary.
+#include "rt_capi.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "rt_internal.hpp"
+
+#pragma clang fp contract(off)
+
+using namespace rtamd;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+rt_status fail(rt_status st, const std::string& msg) {
+    g_last_error = msg;
+    return st;
+}
+
+rt_status hip_fail(hipError_t e, const char* what) {
+    return fail(e == hipErrorOutOfMemory ? RT_ERR_OOM : RT_ERR_HIP,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define RT_HIP(call)                                    \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #call); \
+    } while (0)
+
+struct DeviceBuffer {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&ptr, need);
+        if (e == hipSuccess) bytes = need;
+        return e;
+    }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+};
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+struct rt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    size_t lds_limit = 0;
+    DeviceBuffer out64, out32, ldr, tm_in, tm_out, dbg;
+    DeviceBuffer counters;  // 2 x u64
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
+    double timed_ms = 0.0;
+    uint64_t launches = 0;
+};
+
+struct rt_scene {
+    rt_context* ctx = nullptr;
+    DeviceBuffer buf;
+    int32_t ns = 0, np = 0, nt = 0, nl = 0;
+    size_t off_sph = 0, off_sph_mat = 0, off_pl = 0, off_pl_mat = 0, off_tri = 0, off_tri_mat = 0,
+           off_lt = 0;
+    bool any_transparent = false;
+    double max_specular = 0.0;  // NaN-aware: stored as +inf when a NaN specular exists
+    bool has_area = false;
+    rt_area_light area{};
+};
+
+namespace {
+
+void pack_material(const rt_material& m, double* o) {
+    o[0] = m.color[0];
+    o[1] = m.color[1];
+    o[2] = m.color[2];
+    o[3] = m.shininess;
+    o[4] = m.specular;
+    o[5] = m.transparency;
+    o[6] = m.refractive_index;
+    o[7] = 0.0;
+}
+
+// Vec3::normalize (Math.h:31-37) on the host (used for the triangle normal, Shape.h:222-227).
+void normalize3(const double* a, double* o) {
+    const double len = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    if (len <= 1e-12) {
+        o[0] = o[1] = o[2] = 0.0;
+        return;
+    }
+    o[0] = a[0] / len;
+    o[1] = a[1] / len;
+    o[2] = a[2] / len;
+}
+
+rt_status harvest_events(rt_context* ctx, bool all) {
+    size_t keep_from = 0;
+    for (size_t i = 0; i < ctx->pending.size(); ++i) {
+        auto& ev = ctx->pending[i];
+        if (!all && hipEventQuery(ev.second) != hipSuccess) {
+            keep_from = i;
+            break;
+        }
+        RT_HIP(hipEventSynchronize(ev.second));
+        float ms = 0.f;
+        RT_HIP(hipEventElapsedTime(&ms, ev.first, ev.second));
+        ctx->timed_ms += ms;
+        ctx->launches += 1;
+        ctx->free_events.push_back(ev);
+        keep_from = i + 1;
+    }
+    ctx->pending.erase(ctx->pending.begin(), ctx->pending.begin() + keep_from);
+    return RT_OK;
+}
+
+rt_status validate_camera(const rt_camera* cam) {
+    if (!cam) return fail(RT_ERR_INVALID_ARG, "camera is NULL");
+    if (cam->width == 0 || cam->height == 0)
+        return fail(RT_ERR_INVALID_ARG, "camera width/height must be > 0");
+    if (cam->aa_samples < 0) return fail(RT_ERR_INVALID_ARG, "aa_samples must be >= 0");
+    if (static_cast<uint64_t>(cam->width) * cam->height > (1ull << 31))
+        return fail(RT_ERR_UNSUPPORTED, "image larger than 2^31 pixels");
+    return RT_OK;
+}
+
+rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
+                       const rt_render_opts* opts_in, TraceParams& p, int& path, bool& lds,
+                       size_t& lds_bytes, uint32_t& rows) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARG, "context is NULL");
+    if (!sc) return fail(RT_ERR_INVALID_ARG, "scene is NULL");
+    if (sc->ctx != ctx) return fail(RT_ERR_INVALID_ARG, "scene belongs to another context");
+    rt_status st = validate_camera(cam);
+    if (st != RT_OK) return st;
+    rt_render_opts opts;
+    if (opts_in) opts = *opts_in;
+    else rt_render_opts_default(&opts);
+    const uint32_t r0 = opts.row_begin;
+    const uint32_t r1 = opts.row_end ? opts.row_end : cam->height;
+    if (r1 > cam->height || r0 >= r1)
+        return fail(RT_ERR_INVALID_ARG, "row range [" + std::to_string(r0) + "," +
+                                            std::to_string(r1) + ") invalid for height " +
+                                            std::to_string(cam->height));
+    if (opts.tonemap < RT_TONEMAP_NONE || opts.tonemap >= RT_TONEMAP_COUNT)
+        return fail(RT_ERR_INVALID_ARG, "tonemap operator out of range");
+    rows = r1 - r0;
+
+    const double* base = static_cast<const double*>(sc->buf.ptr);
+    std::memset(&p, 0, sizeof p);
+    p.sph = base + sc->off_sph;
+    p.sph_mat = base + sc->off_sph_mat;
+    p.pl = base + sc->off_pl;
+    p.pl_mat = base + sc->off_pl_mat;
+    p.tri = base + sc->off_tri;
+    p.tri_mat = base + sc->off_tri_mat;
+    p.lt = base + sc->off_lt;
+    p.ns = sc->ns;
+    p.np = sc->np;
+    p.nt = sc->nt;
+    p.nl = sc->nl;
+    if (sc->has_area && sc->area.samples > 0) {
+        const rt_area_light& a = sc->area;
+        const int k = static_cast<int>(std::lround(std::sqrt(static_cast<double>(a.samples))));
+        if (k * k != a.samples)
+            return fail(RT_ERR_INVALID_ARG, "area light samples must be a perfect square");
+        const double li = a.intensity / static_cast<double>(a.samples);
+        for (int i = 0; i < 3; ++i) {
+            p.al_corner[i] = a.corner[i];
+            p.al_u[i] = a.edge_u[i];
+            p.al_v[i] = a.edge_v[i];
+            p.al_E[i] = a.color[i] * li;
+        }
+        p.al_samples = a.samples;
+        p.al_k = k;
+    }
+    for (int i = 0; i < 3; ++i) p.cam_pos[i] = cam->position[i];
+    p.focal = cam->focal;
+    p.width = cam->width;
+    p.height = cam->height;
+    p.aa = cam->aa_samples;
+    p.max_rec = opts.max_recursion;
+    p.bias = opts.bias;
+    p.seed = opts.seed;
+    p.row0 = r0;
+    p.rows = rows;
+    p.tonemap = opts.tonemap;
+
+    // Which TraceRay shape can this scene produce?  (Scene.h:175-195)
+    if (sc->any_transparent) path = kPathTree;
+    else if (!(sc->max_specular <= opts.bias) && opts.max_recursion > 1) path = kPathChain;
+    else path = kPathDirect;
+    if (path != kPathDirect && opts.max_recursion > kMaxDepth)
+        return fail(RT_ERR_UNSUPPORTED, "max_recursion > " + std::to_string(kMaxDepth) +
+                                            " with reflective/transparent materials");
+    lds_bytes = sizeof(double) * (static_cast<size_t>(kSphStride) * sc->ns +
+                                  static_cast<size_t>(kPlStride) * sc->np +
+                                  static_cast<size_t>(kLtStride) * sc->nl);
+    lds = lds_bytes <= ctx->lds_limit;
+    return RT_OK;
+}
+
+rt_status enqueue(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
+                  const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr) {
+    TraceParams p;
+    int path;
+    bool lds;
+    size_t lds_bytes;
+    uint32_t rows;
+    rt_status st = build_params(ctx, sc, cam, opts, p, path, lds, lds_bytes, rows);
+    if (st != RT_OK) return st;
+    p.out64 = d64;
+    p.out32 = d32;
+    p.ldr = dldr;
+    const int flags = opts ? opts->flags : 0;
+    if (!dldr) p.tonemap = RT_TONEMAP_NONE;
+    if (dldr && p.tonemap == RT_TONEMAP_NONE) p.ldr = nullptr;
+
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+    if (flags & RT_FLAG_TIME_KERNEL) {
+        if (ctx->pending.size() >= 1024) {
+            st = harvest_events(ctx, false);
+            if (st != RT_OK) return st;
+        }
+        if (!ctx->free_events.empty()) {
+            ev = ctx->free_events.back();
+            ctx->free_events.pop_back();
+        } else {
+            RT_HIP(hipEventCreate(&ev.first));
+            RT_HIP(hipEventCreate(&ev.second));
+        }
+        RT_HIP(hipEventRecord(ev.first, ctx->stream));
+    }
+    RT_HIP(launch_trace(p, path, false, lds, lds_bytes, ctx->stream));
+    if (flags & RT_FLAG_TIME_KERNEL) {
+        RT_HIP(hipEventRecord(ev.second, ctx->stream));
+        ctx->pending.push_back(ev);
+    }
+    if (flags & RT_FLAG_COUNT_RAYS) {
+        // Counting variant: same trace with wave-reduced atomics, outputs discarded.
+        TraceParams pc = p;
+        pc.out64 = nullptr;
+        pc.out32 = nullptr;
+        pc.ldr = nullptr;
+        pc.counters = static_cast<unsigned long long*>(ctx->counters.ptr);
+        RT_HIP(launch_trace(pc, path, true, lds, lds_bytes, ctx->stream));
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void rt_render_opts_default(rt_render_opts* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof *o);
+    o->max_recursion = 10;         // Scene.h:24
+    o->tonemap = RT_TONEMAP_ACES;  // RaytracingEngine.cpp:301 tonemap()
+    o->bias = 1e-3;                // Scene.h:291
+    o->seed = 0x5EEDull;
+}
+
+rt_status rt_context_create(int device, rt_context** out) {
+    if (!out) return fail(RT_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(RT_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n)
+        return fail(RT_ERR_NO_DEVICE, "device " + std::to_string(device) + " not in [0," +
+                                          std::to_string(n) + ")");
+    hipDeviceProp_t prop;
+    RT_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(RT_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName +
+                                          ", this build targets gfx950 only");
+    DeviceGuard g(device);
+    rt_context* ctx = new (std::nothrow) rt_context();
+    if (!ctx) return fail(RT_ERR_OOM, "host allocation failed");
+    ctx->device = device;
+    // stay at <= 40 KiB of staged scene per 256-thread workgroup so >= 4 workgroups fit a CU
+    ctx->lds_limit = 40 * 1024;
+    hipError_t e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = ctx->counters.ensure(2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(ctx->counters.ptr, 0, 2 * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        rt_context_destroy(ctx);
+        return hip_fail(e, "rt_context_create");
+    }
+    ctx->stream = ctx->own_stream;
+    *out = ctx;
+    return RT_OK;
+}
+
+rt_status rt_context_destroy(rt_context* ctx) {
+    if (!ctx) return RT_OK;
+    DeviceGuard g(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto* v : {&ctx->pending, &ctx->free_events})
+        for (auto& ev : *v) {
+            (void)hipEventDestroy(ev.first);
+            (void)hipEventDestroy(ev.second);
+        }
+    for (DeviceBuffer* b : {&ctx->out64, &ctx->out32, &ctx->ldr, &ctx->tm_in, &ctx->tm_out,
+                            &ctx->dbg, &ctx->counters})
+        b->release();
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return RT_OK;
+}
+
+rt_status rt_context_set_stream(rt_context* ctx, void* hip_stream) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARG, "context is NULL");
+    ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+    return RT_OK;
+}
+
+rt_status rt_context_synchronize(rt_context* ctx) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARG, "context is NULL");
+    DeviceGuard g(ctx->device);
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+rt_status rt_scene_create(rt_context* ctx, const rt_scene_desc* d, rt_scene** out) {
+    if (!ctx || !d || !out) return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_scene_create");
+    *out = nullptr;
+    if (d->n_spheres < 0 || d->n_planes < 0 || d->n_triangles < 0 || d->n_lights < 0)
+        return fail(RT_ERR_INVALID_ARG, "negative primitive count");
+    if ((d->n_spheres && !d->spheres) || (d->n_planes && !d->planes) ||
+        (d->n_triangles && !d->triangles) || (d->n_lights && !d->lights))
+        return fail(RT_ERR_INVALID_ARG, "primitive count > 0 with NULL array");
+    DeviceGuard g(ctx->device);
+
+    rt_scene* sc = new (std::nothrow) rt_scene();
+    if (!sc) return fail(RT_ERR_OOM, "host allocation failed");
+    sc->ctx = ctx;
+    sc->ns = d->n_spheres;
+    sc->np = d->n_planes;
+    sc->nt = d->n_triangles;
+    sc->nl = d->n_lights;
+    size_t off = 0;
+    auto take = [&off](size_t n) {
+        size_t o = off;
+        off += (n + 1) & ~size_t(1);  // keep every array 16-byte aligned
+        return o;
+    };
+    sc->off_sph = take(size_t(kSphStride) * sc->ns);
+    sc->off_sph_mat = take(size_t(kMatStride) * sc->ns);
+    sc->off_pl = take(size_t(kPlStride) * sc->np);
+    sc->off_pl_mat = take(size_t(kMatStride) * sc->np);
+    sc->off_tri = take(size_t(kTriStride) * sc->nt);
+    sc->off_tri_mat = take(size_t(kMatStride) * sc->nt);
+    sc->off_lt = take(size_t(kLtStride) * sc->nl);
+    std::vector<double> h(off + 2, 0.0);
+
+    bool transparent = false;
+    double max_spec = 0.0;
+    auto note = [&](const rt_material& m) {
+        if (!(m.transparency <= 0.0)) transparent = true;
+        if (std::isnan(m.specular)) max_spec = INFINITY;
+        else if (m.specular > max_spec) max_spec = m.specular;
+    };
+    for (int i = 0; i < sc->ns; ++i) {
+        const rt_sphere& s = d->spheres[i];
+        double* o = &h[sc->off_sph + size_t(kSphStride) * i];
+        o[0] = s.center[0];
+        o[1] = s.center[1];
+        o[2] = s.center[2];
+        o[3] = s.radius * s.radius;  // Shape.h:77
+        pack_material(s.material, &h[sc->off_sph_mat + size_t(kMatStride) * i]);
+        note(s.material);
+    }
+    for (int i = 0; i < sc->np; ++i) {
+        const rt_plane& pl = d->planes[i];
+        double* o = &h[sc->off_pl + size_t(kPlStride) * i];
+        for (int k = 0; k < 3; ++k) {
+            o[k] = pl.point[k];
+            o[3 + k] = pl.normal[k];
+        }
+        pack_material(pl.material, &h[sc->off_pl_mat + size_t(kMatStride) * i]);
+        note(pl.material);
+    }
+    for (int i = 0; i < sc->nt; ++i) {
+        const rt_triangle& t = d->triangles[i];
+        double* o = &h[sc->off_tri + size_t(kTriStride) * i];
+        double a0[3], a1[3], a2[3], e1u[3], e2u[3], n[3];
+        for (int k = 0; k < 3; ++k) {
+            a0[k] = t.v0[k] + t.translation[k];  // tv0() Shape.h:198
+            a1[k] = t.v1[k] + t.translation[k];
+            a2[k] = t.v2[k] + t.translation[k];
+            e1u[k] = t.v1[k] - t.v0[k];          // untranslated edges for the normal
+            e2u[k] = t.v2[k] - t.v0[k];
+        }
+        const double c[3] = {e1u[1] * e2u[2] - e1u[2] * e2u[1], e1u[2] * e2u[0] - e1u[0] * e2u[2],
+                             e1u[0] * e2u[1] - e1u[1] * e2u[0]};
+        normalize3(c, n);
+        for (int k = 0; k < 3; ++k) {
+            o[k] = a0[k];
+            o[3 + k] = a1[k] - a0[k];  // edge1 = tv1() - a0
+            o[6 + k] = a2[k] - a0[k];  // edge2 = tv2() - a0
+            o[9 + k] = n[k];
+        }
+        pack_material(t.material, &h[sc->off_tri_mat + size_t(kMatStride) * i]);
+        note(t.material);
+    }
+    for (int i = 0; i < sc->nl; ++i) {
+        const rt_light& l = d->lights[i];
+        double* o = &h[sc->off_lt + size_t(kLtStride) * i];
+        for (int k = 0; k < 3; ++k) {
+            o[k] = l.position[k];
+            o[3 + k] = l.color[k] * l.intensity;  // Scene.h:110 emitted
+        }
+    }
+    sc->any_transparent = transparent;
+    sc->max_specular = max_spec;
+
+    hipError_t e = sc->buf.ensure(h.size() * sizeof(double));
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(sc->buf.ptr, h.data(), h.size() * sizeof(double),
+                           hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        sc->buf.release();
+        delete sc;
+        return hip_fail(e, "rt_scene_create upload");
+    }
+    *out = sc;
+    return RT_OK;
+}
+
+rt_status rt_scene_destroy(rt_scene* sc) {
+    if (!sc) return RT_OK;
+    DeviceGuard g(sc->ctx->device);
+    (void)hipStreamSynchronize(sc->ctx->stream);
+    sc->buf.release();
+    delete sc;
+    return RT_OK;
+}
+
+rt_status rt_scene_set_area_light(rt_scene* sc, const rt_area_light* light) {
+    if (!sc) return fail(RT_ERR_INVALID_ARG, "scene is NULL");
+    if (!light) {
+        sc->has_area = false;
+        return RT_OK;
+    }
+    if (light->samples <= 0) return fail(RT_ERR_INVALID_ARG, "area light needs samples > 0");
+    const int k = static_cast<int>(std::lround(std::sqrt(static_cast<double>(light->samples))));
+    if (k * k != light->samples)
+        return fail(RT_ERR_INVALID_ARG, "area light samples must be a perfect square");
+    sc->area = *light;
+    sc->has_area = true;
+    return RT_OK;
+}
+
+rt_status rt_render_device(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
+                           const rt_render_opts* opts, void* d64, void* d32, void* dldr) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARG, "context is NULL");
+    DeviceGuard g(ctx->device);
+    return enqueue(ctx, sc, cam, opts, static_cast<double*>(d64), static_cast<float*>(d32),
+                   static_cast<uint8_t*>(dldr));
+}
+
+rt_status rt_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
+                    const rt_render_opts* opts, double* h64, float* h32, uint8_t* hldr,
+                    rt_stats* stats) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARG, "context is NULL");
+    rt_status st = validate_camera(cam);
+    if (st != RT_OK) return st;
+    DeviceGuard g(ctx->device);
+    rt_render_opts o;
+    if (opts) o = *opts;
+    else rt_render_opts_default(&o);
+    if (stats) o.flags |= RT_FLAG_COUNT_RAYS;
+    const uint32_t r1 = o.row_end ? o.row_end : cam->height;
+    const uint32_t rows = r1 > o.row_begin ? r1 - o.row_begin : 0;
+    const size_t npx = static_cast<size_t>(rows) * cam->width;
+    if (h64) RT_HIP(ctx->out64.ensure(npx * 3 * sizeof(double)));
+    if (h32) RT_HIP(ctx->out32.ensure(npx * 3 * sizeof(float)));
+    if (hldr) RT_HIP(ctx->ldr.ensure(npx * 3));
+    if (stats) {
+        RT_HIP(hipMemsetAsync(ctx->counters.ptr, 0, 2 * sizeof(unsigned long long), ctx->stream));
+    }
+    st = enqueue(ctx, sc, cam, &o, h64 ? static_cast<double*>(ctx->out64.ptr) : nullptr,
+                 h32 ? static_cast<float*>(ctx->out32.ptr) : nullptr,
+                 hldr ? static_cast<uint8_t*>(ctx->ldr.ptr) : nullptr);
+    if (st != RT_OK) return st;
+    if (h64)
+        RT_HIP(hipMemcpyAsync(h64, ctx->out64.ptr, npx * 3 * sizeof(double),
+                              hipMemcpyDeviceToHost, ctx->stream));
+    if (h32)
+        RT_HIP(hipMemcpyAsync(h32, ctx->out32.ptr, npx * 3 * sizeof(float),
+                              hipMemcpyDeviceToHost, ctx->stream));
+    if (hldr)
+        RT_HIP(hipMemcpyAsync(hldr, ctx->ldr.ptr, npx * 3, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        unsigned long long c[2] = {0, 0};
+        RT_HIP(hipMemcpy(c, ctx->counters.ptr, sizeof c, hipMemcpyDeviceToHost));
+        stats->trace_rays = c[0];
+        stats->shadow_rays = c[1];
+        if (o.flags & RT_FLAG_TIME_KERNEL) {
+            st = harvest_events(ctx, true);
+            if (st != RT_OK) return st;
+            stats->kernel_ms = ctx->timed_ms;
+            stats->launches = ctx->launches;
+        }
+    }
+    return RT_OK;
+}
+
+rt_status rt_stats_read(rt_context* ctx, rt_stats* out) {
+    if (!ctx || !out) return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_stats_read");
+    DeviceGuard g(ctx->device);
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    rt_status st = harvest_events(ctx, true);
+    if (st != RT_OK) return st;
+    unsigned long long c[2] = {0, 0};
+    RT_HIP(hipMemcpy(c, ctx->counters.ptr, sizeof c, hipMemcpyDeviceToHost));
+    out->trace_rays = c[0];
+    out->shadow_rays = c[1];
+    out->kernel_ms = ctx->timed_ms;
+    out->launches = ctx->launches;
+    return RT_OK;
+}
+
+rt_status rt_stats_reset(rt_context* ctx) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARG, "context is NULL");
+    DeviceGuard g(ctx->device);
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    rt_status st = harvest_events(ctx, true);
+    if (st != RT_OK) return st;
+    ctx->timed_ms = 0.0;
+    ctx->launches = 0;
+    RT_HIP(hipMemset(ctx->counters.ptr, 0, 2 * sizeof(unsigned long long)));
+    return RT_OK;
+}
+
+rt_status rt_tonemap(rt_context* ctx, const double* hdr, size_t n, int op, uint8_t* out) {
+    if (!ctx || (!hdr && n) || (!out && n))
+        return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_tonemap");
+    if (op < 0 || op > RT_TONEMAP_COUNT) return fail(RT_ERR_INVALID_ARG, "tonemap op out of range");
+    if (n == 0) return RT_OK;
+    DeviceGuard g(ctx->device);
+    const size_t planes = op == RT_TONEMAP_COUNT ? RT_TONEMAP_COUNT : 1;
+    RT_HIP(ctx->tm_in.ensure(n * 3 * sizeof(double)));
+    RT_HIP(ctx->tm_out.ensure(planes * n * 3));
+    RT_HIP(hipMemcpyAsync(ctx->tm_in.ptr, hdr, n * 3 * sizeof(double), hipMemcpyHostToDevice,
+                          ctx->stream));
+    RT_HIP(launch_tonemap(static_cast<const double*>(ctx->tm_in.ptr), n, op,
+                          static_cast<uint8_t*>(ctx->tm_out.ptr), ctx->stream));
+    RT_HIP(hipMemcpyAsync(out, ctx->tm_out.ptr, planes * n * 3, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+rt_status rt_debug_f64_ops(rt_context* ctx, const double* x, const double* y, size_t n,
+                           double* out) {
+    if (!ctx || !x || !y || !out) return fail(RT_ERR_INVALID_ARG, "NULL argument");
+    DeviceGuard g(ctx->device);
+    RT_HIP(ctx->dbg.ensure(n * 6 * sizeof(double)));
+    double* dx = static_cast<double*>(ctx->dbg.ptr);
+    double* dy = dx + n;
+    double* dout = dy + n;
+    RT_HIP(hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    RT_HIP(hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    RT_HIP(launch_debug_f64(dx, dy, n, dout, ctx->stream));
+    RT_HIP(hipMemcpyAsync(out, dout, 4 * n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+}  // extern "C"

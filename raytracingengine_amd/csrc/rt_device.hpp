@@ -1,0 +1,144 @@
+// rt_device.hpp — gfx950 device-side FP64 vector math for the trace kernels.
+//
+// Every helper evaluates in the same operation order as the reference's Vec3
+// (/root/reference/RaytracingEngine/Math.h:9-71), and the whole library is compiled with
+// -ffp-contract=off (and the pragma below), so no multiply-add is fused and every rounding
+// matches the reference's x86-64 SSE2 build.  Device double division and sqrt lower to the
+// correctly rounded gfx950 sequences (pinned by tests/test_gpu_parity.py::test_device_libm).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace rtamd {
+
+struct d3 {
+    double x, y, z;
+};
+
+__device__ __forceinline__ d3 mk(double x, double y, double z) { return d3{x, y, z}; }
+__device__ __forceinline__ d3 operator+(d3 a, d3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ d3 operator-(d3 a, d3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ d3 operator*(d3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ d3 operator-(d3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ d3 hmul(d3 a, d3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ d3 hdiv(d3 a, d3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
+__device__ __forceinline__ d3 sdiv(d3 a, double s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ d3 sadd(d3 a, double s) { return {a.x + s, a.y + s, a.z + s}; }
+__device__ __forceinline__ d3 ssub(d3 a, double s) { return {a.x - s, a.y - s, a.z - s}; }
+// Vec3::dot — ((x*x' + y*y') + z*z')
+__device__ __forceinline__ double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ d3 cross(d3 a, d3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ double length(d3 a) { return sqrt(dot(a, a)); }
+// Vec3::normalize: zero vector below 1e-12, otherwise three true divisions.
+__device__ __forceinline__ d3 unit(d3 a) {
+    const double l = length(a);
+    if (l <= 1e-12) return {0.0, 0.0, 0.0};
+    return sdiv(a, l);
+}
+// std::max / std::min / std::clamp with libstdc++'s comparison order (NaN handling).
+__device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
+__device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }
+__device__ __forceinline__ double sclamp(double v, double lo, double hi) {
+    return (v < lo) ? lo : (hi < v) ? hi : v;
+}
+// Vec3::reflect: this - (n * 2.0) * dot(this, n)
+__device__ __forceinline__ d3 reflect(d3 i, d3 n) { return i - (n * 2.0) * dot(i, n); }
+// Vec3::refract (Math.h:43-52)
+__device__ __forceinline__ d3 refract(d3 v, d3 n, double eta) {
+    const d3 I = unit(v);
+    const d3 N = unit(n);
+    const double cosi = sclamp(dot(I, N), -1.0, 1.0);
+    const double k = 1.0 - eta * eta * (1.0 - cosi * cosi);
+    if (k < 0.0) return {0.0, 0.0, 0.0};
+    return I * eta - N * (eta * cosi + sqrt(k));
+}
+
+// Build-defined counter RNG (the reference's jitter is an unseeded mt19937, Math.h:109-112).
+// Identical integer arithmetic to oracle_u01 so AA>1 and area-light renders are reproducible.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double u01(uint64_t seed, uint64_t pixel, uint32_t stream,
+                                      uint32_t index) {
+    uint64_t h = mix64(seed ^ (0x9E3779B97F4A7C15ULL * (pixel + 1ULL)));
+    h = mix64(h ^ ((static_cast<uint64_t>(stream) << 32) | index));
+    return static_cast<double>(h >> 11) * 0x1.0p-53;
+}
+
+// Sky colour, Scene::backgroundColor (Scene.h:30-33).
+__device__ __forceinline__ d3 sky(d3 dir) {
+    const double t = 0.5 * (unit(dir).y + 1.0);
+    return mk(1.0, 1.0, 1.0) * (1.0 - t) + mk(0.5, 0.7, 1.0) * t;
+}
+
+// ------------------------------------------------------------------ tonemap operators
+// RaytracingEngine.cpp:70-174.  Float literals are float-rounded then promoted, and the
+// products/quotients of two float constants are formed in float, exactly as the reference.
+__device__ __forceinline__ d3 clamp3(d3 v, double lo, double hi) {
+    return {smin(hi, smax(lo, v.x)), smin(hi, smax(lo, v.y)), smin(hi, smax(lo, v.z))};
+}
+__device__ __forceinline__ d3 uncharted2_partial(d3 x) {
+    const float A = 0.15f, B = 0.50f, C = 0.10f, D = 0.20f, E = 0.02f, F = 0.30f;
+    const float CB = C * B, DE = D * E, DF = D * F, EF = E / F;
+    const d3 num = sadd(hmul(x, sadd(x * static_cast<double>(A), static_cast<double>(CB))),
+                        static_cast<double>(DE));
+    const d3 den = sadd(hmul(x, sadd(x * static_cast<double>(A), static_cast<double>(B))),
+                        static_cast<double>(DF));
+    return ssub(hdiv(num, den), static_cast<double>(EF));
+}
+__device__ __forceinline__ double luminance(d3 c) { return dot(c, mk(0.2126, 0.7152, 0.0722)); }
+__device__ __forceinline__ d3 change_luminance(d3 c, double l_out) {
+    return c * (l_out / luminance(c));
+}
+__device__ __forceinline__ d3 tonemap_op(d3 c, int op) {
+    switch (op) {
+    case 0:  // simple
+        return {smin(1.0, smax(0.0, c.x)), smin(1.0, smax(0.0, c.y)), smin(1.0, smax(0.0, c.z))};
+    case 1:  // reinhardSimple: c / (c + 1)
+        return hdiv(c, sadd(c, 1.0));
+    case 2: {  // reinhardExtended(c, 5.0)
+        const double ws = 5.0 * 5.0;
+        return hdiv(hmul(c, sadd(hdiv(c, mk(ws, ws, ws)), 1.0)), sadd(c, 1.0));
+    }
+    case 3: {  // reinhardExtendedLuminance(c, 5.0)
+        const double lo = luminance(c);
+        const double num = lo * (1.0 + (lo / (5.0 * 5.0)));
+        return change_luminance(c, num / (1.0 + lo));
+    }
+    case 4: {  // reinhardJodie(c, 0.18)
+        const double L = luminance(c);
+        const double lm = (0.18 / log(2.0 + pow((L / 0.85), 1.7))) * log(1.0 + L);
+        return change_luminance(c, lm);
+    }
+    case 5: {  // uncharted2
+        const double exposure = static_cast<double>(2.0f);
+        const d3 cur = uncharted2_partial(c * exposure);
+        const d3 ws = hdiv(mk(1.0, 1.0, 1.0), uncharted2_partial(mk(11.2, 11.2, 11.2)));
+        return hmul(cur, ws);
+    }
+    default: {  // aces_approx
+        const d3 v = c * static_cast<double>(0.6f);
+        const float a = 2.51f, b = 0.03f, cc = 2.43f, d = 0.59f, e = 0.14f;
+        const d3 num = hmul(v, sadd(v * static_cast<double>(a), static_cast<double>(b)));
+        const d3 den = sadd(hmul(v, sadd(v * static_cast<double>(cc), static_cast<double>(d))),
+                            static_cast<double>(e));
+        return clamp3(hdiv(num, den), static_cast<double>(0.0f), static_cast<double>(1.0f));
+    }
+    }
+}
+// toColor (RaytracingEngine.cpp:113-121): clamp to [0,1], truncating cast of x*255.
+__device__ __forceinline__ void to_color(d3 v, uint8_t& r, uint8_t& g, uint8_t& b) {
+    const d3 c = clamp3(v, 0.0, 1.0);
+    r = static_cast<uint8_t>(c.x * 255.0);
+    g = static_cast<uint8_t>(c.y * 255.0);
+    b = static_cast<uint8_t>(c.z * 255.0);
+}
+
+}  // namespace rtamd

@@ -1,0 +1,71 @@
+// rt_internal.hpp — what the C-ABI layer (rt_capi.cpp) and the kernels (rt_trace.hip) share.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace rtamd {
+
+// Device scene records (doubles per record).  Layout in HBM is one allocation, record arrays
+// back to back; the per-ray geometry arrays (sphere/plane/light) are staged into LDS.
+constexpr int kSphStride = 4;   // cx cy cz r²            (r² = radius*radius, as Shape.h:77)
+constexpr int kPlStride = 8;    // px py pz nx ny nz - -  (normal as stored, Shape.h:142)
+constexpr int kTriStride = 12;  // a0(3) e1(3) e2(3) n(3) (translated v0 and edges, Shape.h:204-206;
+                                //                         untranslated normal, Shape.h:222-227)
+constexpr int kLtStride = 8;    // px py pz Ex Ey Ez - -  (E = color*intensity, Scene.h:110)
+constexpr int kMatStride = 8;   // r g b shininess specular transparency ior -
+
+constexpr int kMaxDepth = 16;   // deepest recursion the CHAIN/TREE kernels keep a stack for
+constexpr int kTileW = 64;      // pixels per wave along a row (one wave = 64 contiguous pixels)
+constexpr int kTileH = 4;       // rows per workgroup (256 threads)
+
+enum PathKind : int {
+    kPathDirect = 0,  // no material can spawn a secondary ray: primary + shadow rays only
+    kPathChain = 1,   // opaque, some specular > bias: linear reflection chain (≤ maxRecursion)
+    kPathTree = 2     // some transparency > 0: refraction + reflection binary tree
+};
+
+struct TraceParams {
+    // scene (device pointers into the scene allocation)
+    const double* sph;
+    const double* sph_mat;
+    const double* pl;
+    const double* pl_mat;
+    const double* tri;
+    const double* tri_mat;
+    const double* lt;
+    int32_t ns, np, nt, nl;
+    // build-defined area light (samples == 0: none)
+    double al_corner[3];
+    double al_u[3];
+    double al_v[3];
+    double al_E[3];        // color * (intensity / samples)
+    int32_t al_samples;
+    int32_t al_k;          // sqrt(samples)
+    // camera
+    double cam_pos[3];
+    double focal;
+    uint32_t width, height;
+    int32_t aa;
+    int32_t max_rec;
+    double bias;
+    uint64_t seed;
+    // tile
+    uint32_t row0, rows;
+    // outputs (device; any may be null)
+    double* out64;
+    float* out32;
+    uint8_t* ldr;
+    int32_t tonemap;
+    int32_t _pad;
+    unsigned long long* counters;  // [trace, shadow] — only written by the counting variant
+};
+
+hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
+                        hipStream_t stream);
+hipError_t launch_tonemap(const double* hdr, size_t n, int op, uint8_t* out, hipStream_t stream);
+hipError_t launch_debug_f64(const double* x, const double* y, size_t n, double* out,
+                            hipStream_t stream);
+
+}  // namespace rtamd
