@@ -207,6 +207,19 @@ rt_status rt_render_device(rt_context* ctx, const rt_scene* scene, const rt_came
 rt_status rt_stats_read(rt_context* ctx, rt_stats* out);
 rt_status rt_stats_reset(rt_context* ctx);
 
+/* Batch Scene::TraceRay (Scene.h:131-198) at recursion depth 0 for n arbitrary host rays
+ * {ox,oy,oz,dx,dy,dz}: the per-sample body of GenerateAntiAliasing (Scene.h:306-309).
+ * rgb_out: n*3 doubles.  opts->max_recursion/bias/seed apply; the area-light RNG is keyed by
+ * the ray's index.  stats may be NULL. */
+rt_status rt_trace_rays(rt_context* ctx, const rt_scene* scene, const rt_render_opts* opts,
+                        const double* rays, size_t n, double* rgb_out, rt_stats* stats);
+
+/* Batch Scene::IntersectClosest (Scene.h:218-257) for n host rays.  hits_out: n*9 doubles
+ * {type, index, distance, normal.xyz, hitPoint.xyz}; type 0 = miss (index -1), 1 sphere,
+ * 2 plane, 3 triangle (index into rt_scene_desc.triangles). */
+rt_status rt_intersect_rays(rt_context* ctx, const rt_scene* scene, const double* rays,
+                            size_t n, double* hits_out);
+
 /* Device tonemap of host FP64 radiance: op in [0, RT_TONEMAP_COUNT) writes n*3 bytes;
  * op == RT_TONEMAP_COUNT writes all seven operators, tonemapAll() order, 7*n*3 bytes. */
 rt_status rt_tonemap(rt_context* ctx, const double* hdr, size_t n_pixels, int op,

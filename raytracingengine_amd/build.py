@@ -47,9 +47,44 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+API_DIR = os.path.join(HERE, "api")
+CPP_LIB = os.path.join(HERE, "librtamd_cpp.so")
+CPP_FLAGS = ["-std=c++20", "-O2", "-fPIC", "-ffp-contract=off", "-Wall", "-Wextra",
+             f"-I{API_DIR}", f"-I{os.path.join(ROOT, 'include')}"]
+EXAMPLES = {"box_demo": "box_demo.cpp", "render_scenefile": "render_scenefile.cpp"}
+
+
+def build_cpp_api(force: bool = False, verbose: bool = False) -> str:
+    """The drop-in C++20 API (api/rtamd/*.cpp) as librtamd_cpp.so over librtamd.so, plus the
+    example programs under examples/ (bin in examples/bin, rpath to the package dir)."""
+    build_library(force=force, verbose=verbose)
+    srcs = [os.path.join(API_DIR, "rtamd", f) for f in ("scene.cpp", "image.cpp")]
+    hdrs = [os.path.join(API_DIR, "rtamd", f) for f in os.listdir(os.path.join(API_DIR, "rtamd"))]
+    link = [f"-L{HERE}", "-lrtamd", f"-Wl,-rpath,{HERE}", "-Wl,-rpath,$ORIGIN"]
+    cxx = os.environ.get("CXX", "g++")
+    if force or _stale(CPP_LIB, srcs + hdrs + [LIB]):
+        cmd = [cxx, *CPP_FLAGS, "-shared", "-o", CPP_LIB, *srcs, *link]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    bindir = os.path.join(ROOT, "examples", "bin")
+    os.makedirs(bindir, exist_ok=True)
+    for exe, src in EXAMPLES.items():
+        src = os.path.join(ROOT, "examples", src)
+        target = os.path.join(bindir, exe)
+        if force or _stale(target, [src, CPP_LIB] + hdrs):
+            cmd = [cxx, *CPP_FLAGS, "-o", target, src, f"-L{HERE}", "-lrtamd_cpp", "-lrtamd",
+                   f"-Wl,-rpath,{HERE}", "-Wl,-rpath,$ORIGIN/../../raytracingengine_amd"]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+    return CPP_LIB
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     print(build_library(force="--force" in argv, verbose=True))
+    print(build_cpp_api(force="--force" in argv, verbose=True))
 
 
 if __name__ == "__main__":

@@ -31,7 +31,8 @@ EXPORTED = [
     "rt_last_error", "rt_device_count", "rt_render_opts_default", "rt_context_create",
     "rt_context_destroy", "rt_context_set_stream", "rt_context_synchronize", "rt_scene_create",
     "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
-    "rt_stats_read", "rt_stats_reset", "rt_tonemap", "rt_debug_f64_ops",
+    "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
+    "rt_debug_f64_ops",
 ]
 
 
@@ -102,6 +103,8 @@ def load_library(path: str = LIB_PATH):
         "rt_render_device": [vp, vp, vp, vp, vp, vp, vp],
         "rt_stats_read": [vp, vp],
         "rt_stats_reset": [vp],
+        "rt_trace_rays": [vp, vp, vp, vp, ctypes.c_size_t, vp, vp],
+        "rt_intersect_rays": [vp, vp, vp, ctypes.c_size_t, vp],
         "rt_tonemap": [vp, vp, ctypes.c_size_t, i32, vp],
         "rt_debug_f64_ops": [vp, vp, vp, ctypes.c_size_t, vp],
     }.items():
@@ -252,6 +255,25 @@ class DeviceScene:
         if stats:
             out["trace_rays"] = st.trace_rays
             out["shadow_rays"] = st.shadow_rays
+        return out
+
+    def trace_rays(self, rays: np.ndarray, stats=False, **opt_kw):
+        """Batch TraceRay at depth 0 (rt_trace_rays): rays [n,6] -> rgb [n,3]."""
+        rays = np.ascontiguousarray(rays, np.float64).reshape(-1, 6)
+        out = np.empty((rays.shape[0], 3), np.float64)
+        o = default_opts(**opt_kw)
+        st = Stats()
+        _check(_lib.rt_trace_rays(self.ctx.handle, self._h, ctypes.byref(o), rays.ctypes.data,
+                                  rays.shape[0], out.ctypes.data,
+                                  ctypes.byref(st) if stats else None))
+        return (out, st) if stats else out
+
+    def intersect_rays(self, rays: np.ndarray) -> np.ndarray:
+        """Batch IntersectClosest (rt_intersect_rays): rays [n,6] -> hits [n,9]."""
+        rays = np.ascontiguousarray(rays, np.float64).reshape(-1, 6)
+        out = np.empty((rays.shape[0], 9), np.float64)
+        _check(_lib.rt_intersect_rays(self.ctx.handle, self._h, rays.ctypes.data, rays.shape[0],
+                                      out.ctypes.data))
         return out
 
     def render_device(self, d_hdr64: int | None, d_hdr32: int | None, d_ldr: int | None,

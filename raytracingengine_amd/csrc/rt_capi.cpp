@@ -79,7 +79,7 @@ struct rt_context {
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     size_t lds_limit = 0;
-    DeviceBuffer out64, out32, ldr, tm_in, tm_out, dbg;
+    DeviceBuffer out64, out32, ldr, tm_in, tm_out, dbg, rays;
     DeviceBuffer counters;  // 2 x u64
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
@@ -217,7 +217,7 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
 
     // Which TraceRay shape can this scene produce?  (Scene.h:175-195)
     if (sc->any_transparent) path = kPathTree;
-    else if (!(sc->max_specular <= opts.bias) && opts.max_recursion > 1) path = kPathChain;
+    else if (!(sc->max_specular <= opts.bias) && opts.max_recursion >= 1) path = kPathChain;
     else path = kPathDirect;
     if (path != kPathDirect && opts.max_recursion > kMaxDepth)
         return fail(RT_ERR_UNSUPPORTED, "max_recursion > " + std::to_string(kMaxDepth) +
@@ -340,7 +340,7 @@ rt_status rt_context_destroy(rt_context* ctx) {
             (void)hipEventDestroy(ev.second);
         }
     for (DeviceBuffer* b : {&ctx->out64, &ctx->out32, &ctx->ldr, &ctx->tm_in, &ctx->tm_out,
-                            &ctx->dbg, &ctx->counters})
+                            &ctx->dbg, &ctx->rays, &ctx->counters})
         b->release();
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -572,6 +572,80 @@ rt_status rt_stats_reset(rt_context* ctx) {
     ctx->timed_ms = 0.0;
     ctx->launches = 0;
     RT_HIP(hipMemset(ctx->counters.ptr, 0, 2 * sizeof(unsigned long long)));
+    return RT_OK;
+}
+
+// A 1×1 camera: the batch entry points reuse build_params for the scene/opts part only.
+static rt_camera batch_camera() {
+    rt_camera c;
+    std::memset(&c, 0, sizeof c);
+    c.width = 1;
+    c.height = 1;
+    c.aa_samples = 1;
+    return c;
+}
+
+rt_status rt_trace_rays(rt_context* ctx, const rt_scene* sc, const rt_render_opts* opts,
+                        const double* rays, size_t n, double* rgb, rt_stats* stats) {
+    if (!ctx || (n && (!rays || !rgb))) return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_trace_rays");
+    DeviceGuard g(ctx->device);
+    const rt_camera cam = batch_camera();
+    rt_render_opts o;
+    if (opts) o = *opts;
+    else rt_render_opts_default(&o);
+    o.row_begin = 0;
+    o.row_end = 0;
+    TraceParams p;
+    int path;
+    bool lds;
+    size_t lds_bytes;
+    uint32_t rows;
+    rt_status st = build_params(ctx, sc, &cam, &o, p, path, lds, lds_bytes, rows);
+    if (st != RT_OK) return st;
+    if (stats) std::memset(stats, 0, sizeof *stats);
+    if (n == 0) return RT_OK;
+    RT_HIP(ctx->rays.ensure(n * 9 * sizeof(double)));
+    double* d_rays = static_cast<double*>(ctx->rays.ptr);
+    double* d_out = d_rays + 6 * n;
+    RT_HIP(hipMemcpyAsync(d_rays, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    RT_HIP(launch_trace_rays(p, path, false, d_rays, n, d_out, ctx->stream));
+    RT_HIP(hipMemcpyAsync(rgb, d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (stats) {
+        p.counters = static_cast<unsigned long long*>(ctx->counters.ptr);
+        RT_HIP(hipMemsetAsync(p.counters, 0, 2 * sizeof(unsigned long long), ctx->stream));
+        RT_HIP(launch_trace_rays(p, path, true, d_rays, n, d_out, ctx->stream));
+        unsigned long long c[2] = {0, 0};
+        RT_HIP(hipMemcpyAsync(c, p.counters, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
+        RT_HIP(hipStreamSynchronize(ctx->stream));
+        stats->trace_rays = c[0];
+        stats->shadow_rays = c[1];
+        return RT_OK;
+    }
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+rt_status rt_intersect_rays(rt_context* ctx, const rt_scene* sc, const double* rays, size_t n,
+                            double* hits) {
+    if (!ctx || (n && (!rays || !hits)))
+        return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_intersect_rays");
+    DeviceGuard g(ctx->device);
+    const rt_camera cam = batch_camera();
+    TraceParams p;
+    int path;
+    bool lds;
+    size_t lds_bytes;
+    uint32_t rows;
+    rt_status st = build_params(ctx, sc, &cam, nullptr, p, path, lds, lds_bytes, rows);
+    if (st != RT_OK) return st;
+    if (n == 0) return RT_OK;
+    RT_HIP(ctx->rays.ensure(n * 15 * sizeof(double)));
+    double* d_rays = static_cast<double*>(ctx->rays.ptr);
+    double* d_out = d_rays + 6 * n;
+    RT_HIP(hipMemcpyAsync(d_rays, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    RT_HIP(launch_intersect_rays(p, d_rays, n, d_out, ctx->stream));
+    RT_HIP(hipMemcpyAsync(hits, d_out, n * 9 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
     return RT_OK;
 }
 

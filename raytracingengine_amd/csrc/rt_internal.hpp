@@ -64,6 +64,10 @@ struct TraceParams {
 
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
                         hipStream_t stream);
+hipError_t launch_trace_rays(const TraceParams& p, int path, bool count, const double* rays,
+                             size_t n, double* out, hipStream_t stream);
+hipError_t launch_intersect_rays(const TraceParams& p, const double* rays, size_t n, double* out,
+                                 hipStream_t stream);
 hipError_t launch_tonemap(const double* hdr, size_t n, int op, uint8_t* out, hipStream_t stream);
 hipError_t launch_debug_f64(const double* x, const double* y, size_t n, double* out,
                             hipStream_t stream);

@@ -535,6 +535,110 @@ hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, si
     }
 }
 
+// ------------------------------------------------------------------ batch ray queries
+__device__ __forceinline__ SceneView global_view(const TraceParams& P) {
+    SceneView S;
+    S.ns = P.ns;
+    S.np = P.np;
+    S.nt = P.nt;
+    S.nl = P.nl;
+    S.sph = P.sph;
+    S.pl = P.pl;
+    S.lt = P.lt;
+    S.tri = P.tri;
+    S.sph_mat = P.sph_mat;
+    S.pl_mat = P.pl_mat;
+    S.tri_mat = P.tri_mat;
+    return S;
+}
+
+// TraceRay(ray, 0, bias) for arbitrary rays (GenerateAntiAliasing's body, Scene.h:306-309).
+template <int PATH, bool COUNT>
+__global__ __launch_bounds__(256) void trace_rays_kernel(TraceParams P, const double* rays,
+                                                         size_t n, double* out) {
+    const SceneView S = global_view(P);
+    const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    Counts cnt{0u, 0u};
+    if (i < n) {
+        const double* r = rays + 6 * i;
+        const d3 o = mk(r[0], r[1], r[2]);
+        const d3 d = mk(r[3], r[4], r[5]);
+        d3 c;
+        if constexpr (PATH == kPathDirect) c = trace_direct<COUNT>(S, P, o, d, i, 0u, cnt);
+        else if constexpr (PATH == kPathChain) c = trace_chain<COUNT>(S, P, o, d, i, 0u, cnt);
+        else c = trace_tree<COUNT>(S, P, o, d, i, 0u, cnt);
+        out[3 * i + 0] = c.x;
+        out[3 * i + 1] = c.y;
+        out[3 * i + 2] = c.z;
+    }
+    if constexpr (COUNT) {
+        uint32_t t = cnt.trace, s = cnt.shadow;
+        for (int off = 32; off > 0; off >>= 1) {
+            t += __shfl_xor(t, off, 64);
+            s += __shfl_xor(s, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(P.counters + 0, static_cast<unsigned long long>(t));
+            atomicAdd(P.counters + 1, static_cast<unsigned long long>(s));
+        }
+    }
+}
+
+// IntersectClosest for arbitrary rays: {type, index, t, normal, hit point} per ray.
+__global__ __launch_bounds__(256) void intersect_rays_kernel(TraceParams P, const double* rays,
+                                                             size_t n, double* out) {
+    const SceneView S = global_view(P);
+    const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* r = rays + 6 * i;
+    const d3 o = mk(r[0], r[1], r[2]);
+    const d3 d = mk(r[3], r[4], r[5]);
+    double* w = out + 9 * i;
+    Hit h;
+    if (!closest(S, o, d, h)) {
+        w[0] = 0.0;
+        w[1] = -1.0;
+        for (int k = 2; k < 9; ++k) w[k] = 0.0;
+        return;
+    }
+    const d3 p = o + d * h.t;
+    const d3 nn = normal_of(S, h, p);
+    w[0] = static_cast<double>(h.kind);
+    w[1] = static_cast<double>(h.idx);
+    w[2] = h.t;
+    w[3] = nn.x;
+    w[4] = nn.y;
+    w[5] = nn.z;
+    w[6] = p.x;
+    w[7] = p.y;
+    w[8] = p.z;
+}
+
+hipError_t launch_trace_rays(const TraceParams& p, int path, bool count, const double* rays,
+                             size_t n, double* out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const dim3 grid(static_cast<unsigned>((n + 255) / 256)), block(256);
+    if (path == kPathDirect) {
+        if (count) hipLaunchKernelGGL((trace_rays_kernel<kPathDirect, true>), grid, block, 0, stream, p, rays, n, out);
+        else hipLaunchKernelGGL((trace_rays_kernel<kPathDirect, false>), grid, block, 0, stream, p, rays, n, out);
+    } else if (path == kPathChain) {
+        if (count) hipLaunchKernelGGL((trace_rays_kernel<kPathChain, true>), grid, block, 0, stream, p, rays, n, out);
+        else hipLaunchKernelGGL((trace_rays_kernel<kPathChain, false>), grid, block, 0, stream, p, rays, n, out);
+    } else {
+        if (count) hipLaunchKernelGGL((trace_rays_kernel<kPathTree, true>), grid, block, 0, stream, p, rays, n, out);
+        else hipLaunchKernelGGL((trace_rays_kernel<kPathTree, false>), grid, block, 0, stream, p, rays, n, out);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_intersect_rays(const TraceParams& p, const double* rays, size_t n, double* out,
+                                 hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(intersect_rays_kernel, dim3(static_cast<unsigned>((n + 255) / 256)),
+                       dim3(256), 0, stream, p, rays, n, out);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ tonemap
 // op in [0,7): one operator; op == 7: all seven in tonemapAll() order (out is 7 planes).
 __global__ __launch_bounds__(256) void tonemap_kernel(const double* __restrict__ hdr, size_t n,

@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ from the UNMODIFIED reference renderer.
+
+Runs only where /root/reference exists (it drives oracle/_ref/ref_harness, built by
+oracle/Makefile from the reference sources where they lie).  Outputs are data only: inputs
+and the reference's outputs for them.  The reference has no tests or fixtures of its own
+(SURVEY.md §4), so these are the pins of the oracle.
+
+    python tests/golden/make_golden.py          # rewrites tests/golden/*.npz / *.json
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import pyoracle as po  # noqa: E402
+from raytracingengine_amd.configs import make_config  # noqa: E402
+
+SMALL = (96, 54)
+SMALL_SCENES = ["c1", "c2", "c3", "c4", "mirror", "glass", "mesh"]
+FULL_SCENES = ["c1", "c2"]  # full BASELINE resolution: sha256 + 1-in-64 subsample
+SUBSAMPLE = 64
+
+
+def scene_hash(sc) -> str:
+    return hashlib.sha256(sc.to_text().encode()).hexdigest()
+
+
+def run(mode, *args):
+    subprocess.run([po.REF_HARNESS, mode, *map(str, args)], check=True, capture_output=True)
+
+
+def kat_inputs(rng: np.random.Generator):
+    n = 4096
+    # spheres: ray origin, direction (not always unit), centre, radius
+    o = rng.uniform(-20, 20, (n, 3))
+    c = rng.uniform(-10, 10, (n, 3))
+    toward = c - o + rng.normal(0, 3, (n, 3))
+    d = toward * rng.choice([1.0, 1.0, 1.0, 0.25, 3.0], (n, 1))
+    r = rng.uniform(0.1, 6, (n, 1))
+    # special rows: origin inside, tangent-ish, pointing away, zero-length direction
+    o[:64] = c[:64] + rng.uniform(-0.5, 0.5, (64, 3))
+    r[:64] = 2.0
+    d[64:128] = -toward[64:128]
+    d[128:136] = 0.0
+    sphere = np.concatenate([o, d, c, r], axis=1)
+
+    # planes: ray, point, unnormalised normal (some parallel rays, some t==0 exactly)
+    m = 2048
+    po_ = rng.uniform(-20, 20, (m, 3))
+    pd = rng.normal(0, 1, (m, 3))
+    pp = rng.uniform(-10, 10, (m, 3))
+    pn = rng.normal(0, 1, (m, 3)) * rng.choice([1.0, 5.0, 0.1], (m, 1))
+    pd[:64] = np.cross(pn[:64], rng.normal(0, 1, (64, 3)))  # parallel to the plane
+    po_[64:128] = pp[64:128]                                # origin on the plane: t == 0
+    pn[128:136] = 0.0                                       # degenerate normal
+    plane = np.concatenate([po_, pd, pp, pn], axis=1)
+
+    # triangles: ray, v0, v1, v2, translation
+    k = 2048
+    tv = rng.uniform(-5, 5, (k, 9))
+    tt = rng.uniform(-3, 3, (k, 3))
+    centroid = (tv[:, 0:3] + tv[:, 3:6] + tv[:, 6:9]) / 3.0 + tt
+    to = rng.uniform(-15, 15, (k, 3))
+    td = centroid - to + rng.normal(0, 2.0, (k, 3))
+    tv[:32, 6:9] = tv[:32, 0:3] + (tv[:32, 3:6] - tv[:32, 0:3]) * 2.0  # degenerate (collinear)
+    tri = np.concatenate([to, td, tv, tt], axis=1)
+
+    # getRay: pos, focal, W, H, x, y
+    g = 512
+    W = rng.integers(1, 4000, g)
+    H = rng.integers(1, 3000, g)
+    getray = np.stack([rng.uniform(-30, 30, g), rng.uniform(-30, 30, g), rng.uniform(-30, 30, g),
+                       rng.uniform(0.5, 3000, g), W, H, rng.integers(0, W), rng.integers(0, H)],
+                      axis=1).astype(np.float64)
+    return {"sphere": sphere, "plane": plane, "triangle": tri, "getray": getray}
+
+
+def tonemap_inputs(rng):
+    n = 1024
+    px = rng.exponential(1.0, (n, 3)) * rng.choice([0.01, 0.3, 1.0, 5.0, 40.0], (n, 1))
+    px[:16] = 0.0                           # black: luminance operators give 0/0 -> NaN -> 0
+    px[16:32] = rng.uniform(-1, 0, (16, 3))  # negative radiance
+    px[32:48] = rng.uniform(0.99, 1.01, (16, 3))
+    px[48:64] = 1e6
+    px[64:80, 0] = 0.0                       # partial zeros
+    # values that sit exactly on the x*255 truncation boundary
+    px[80:336] = (np.arange(256)[:, None] / 255.0) * np.ones((1, 3))
+    return px
+
+
+def main():
+    if not po.ref_available():
+        po.build()
+    assert po.ref_available(), "oracle/_ref/ref_harness missing (needs /root/reference)"
+    rng = np.random.default_rng(20260128)
+    meta = {"generator": "tests/golden/make_golden.py", "reference": "Sorax5/RaytracingEngine",
+            "reference_build": "oracle/Makefile (g++ -std=c++20 -O2 -fopenmp)", "scenes": {}}
+
+    with tempfile.TemporaryDirectory() as td:
+        # ---- whole-image renders at 96x54, AA=1 (deterministic in the reference)
+        arrays = {}
+        for name in SMALL_SCENES:
+            sc = make_config(name, *SMALL)
+            img, _, _ = po.ref_render(sc)
+            arrays[name] = img
+            meta["scenes"][f"{name}_small"] = {"scene_sha256": scene_hash(sc),
+                                               "width": SMALL[0], "height": SMALL[1]}
+        np.savez_compressed(os.path.join(HERE, "renders_small.npz"), **arrays)
+
+        # ---- full-resolution renders: sha256 of the float64 image + a subsample
+        full = {}
+        for name in FULL_SCENES:
+            sc = make_config(name)
+            img, ms, thr = po.ref_render(sc)
+            flat = img.reshape(-1, 3)
+            full[name] = flat[::SUBSAMPLE]
+            meta["scenes"][f"{name}_full"] = {
+                "scene_sha256": scene_hash(sc), "width": sc.camera.width,
+                "height": sc.camera.height, "image_sha256": hashlib.sha256(img.tobytes()).hexdigest(),
+                "subsample_stride": SUBSAMPLE}
+        np.savez_compressed(os.path.join(HERE, "renders_full_subsample.npz"), **full)
+
+        # ---- per-function known answers
+        kats = kat_inputs(rng)
+        kat_out = {}
+        for kind, arr in kats.items():
+            inp = os.path.join(td, f"{kind}.f64")
+            out = os.path.join(td, f"{kind}.out")
+            np.ascontiguousarray(arr, np.float64).tofile(inp)
+            run("kat", kind, inp, len(arr), out)
+            width = {"sphere": 2, "plane": 5, "triangle": 5, "getray": 6}[kind]
+            kat_out[f"{kind}_in"] = arr
+            kat_out[f"{kind}_out"] = np.fromfile(out, np.float64).reshape(len(arr), width)
+
+        # IntersectClosest on the mesh scene (spheres, planes, triangles, models)
+        sc = make_config("mesh", *SMALL)
+        scene_path = os.path.join(td, "mesh.txt")
+        sc.write(scene_path)
+        nr = 1024
+        ro = rng.uniform(-15, 15, (nr, 3))
+        ro[:, 2] = rng.uniform(-25, -5, nr)
+        rd = rng.uniform(-1, 1, (nr, 3))
+        rd[:, 2] = np.abs(rd[:, 2]) + 0.2
+        rays = np.concatenate([ro, rd], axis=1)
+        rays.tofile(os.path.join(td, "rays.f64"))
+        run("closest", scene_path, os.path.join(td, "rays.f64"), nr, os.path.join(td, "cl.out"))
+        kat_out["closest_rays"] = rays
+        kat_out["closest_out"] = np.fromfile(os.path.join(td, "cl.out"), np.float64).reshape(nr, 9)
+        meta["closest_scene_sha256"] = scene_hash(sc)
+
+        # tonemap operators: curves (pre-quantisation) and toColor bytes; tonemapAll + tonemap()
+        px = tonemap_inputs(rng)
+        px.tofile(os.path.join(td, "px.f64"))
+        run("tonemap", os.path.join(td, "px.f64"), len(px), os.path.join(td, "tm.u8"))
+        run("curves", os.path.join(td, "px.f64"), len(px), os.path.join(td, "cv.f64"))
+        kat_out["tonemap_in"] = px
+        kat_out["tonemap_bytes"] = np.fromfile(os.path.join(td, "tm.u8"), np.uint8).reshape(8, len(px), 3)
+        kat_out["tonemap_curves"] = np.fromfile(os.path.join(td, "cv.f64"), np.float64).reshape(7, len(px), 3)
+
+        # writePPM bytes of a 7x5 image
+        raw = rng.integers(0, 256, (5, 7, 3), dtype=np.uint8)
+        raw.tofile(os.path.join(td, "img.u8"))
+        run("ppm", os.path.join(td, "img.u8"), 7, 5, os.path.join(td, "img.ppm"))
+        kat_out["ppm_in"] = raw
+        kat_out["ppm_bytes"] = np.frombuffer(open(os.path.join(td, "img.ppm"), "rb").read(), np.uint8)
+        np.savez_compressed(os.path.join(HERE, "kats.npz"), **kat_out)
+
+    with open(os.path.join(HERE, "golden_meta.json"), "w") as fh:
+        json.dump(meta, fh, indent=1, sort_keys=True)
+    sizes = {f: os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE)
+             if f.endswith((".npz", ".json"))}
+    print(json.dumps(sizes))
+
+
+if __name__ == "__main__":
+    main()
