@@ -23,7 +23,7 @@ ARCH = "gfx950"
 
 HIP_FLAGS = ["-O3", "-std=c++20", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
              "-Wall", "-Wno-unused-result"]
-SOURCES = ["rt_trace.hip", "rt_capi.cpp"]
+SOURCES = ["rt_trace.hip", "rt_packet.hip", "rt_capi.cpp"]
 LIB = os.path.join(HERE, "librtamd.so")
 
 

@@ -25,6 +25,7 @@ TONEMAPS = ["simple", "reinhard_simple", "reinhard_extended", "reinhard_extended
 TONEMAP_ALL = 7
 RT_FLAG_COUNT_RAYS = 0x1
 RT_FLAG_TIME_KERNEL = 0x2
+RT_FLAG_GENERIC_KERNEL = 0x4
 
 # Every symbol include/rt_capi.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED = [

@@ -260,7 +260,15 @@ rt_status enqueue(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
         }
         RT_HIP(hipEventRecord(ev.first, ctx->stream));
     }
-    RT_HIP(launch_trace(p, path, false, lds, lds_bytes, ctx->stream));
+    // Scenes without secondary rays take the packet-culled kernel when its LDS image fits.
+    const bool packet = path == kPathDirect && !(flags & RT_FLAG_GENERIC_KERNEL) &&
+                        p.ns <= packet_max_spheres() &&
+                        packet_lds_bytes(p.ns, p.np, p.nl) <= ctx->lds_limit;
+    auto launch = [&](const TraceParams& q, bool count) {
+        return packet ? launch_packet_direct(q, count, sc->max_specular > 0.0, ctx->stream)
+                      : launch_trace(q, path, count, lds, lds_bytes, ctx->stream);
+    };
+    RT_HIP(launch(p, false));
     if (flags & RT_FLAG_TIME_KERNEL) {
         RT_HIP(hipEventRecord(ev.second, ctx->stream));
         ctx->pending.push_back(ev);
@@ -272,7 +280,7 @@ rt_status enqueue(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
         pc.out32 = nullptr;
         pc.ldr = nullptr;
         pc.counters = static_cast<unsigned long long*>(ctx->counters.ptr);
-        RT_HIP(launch_trace(pc, path, true, lds, lds_bytes, ctx->stream));
+        RT_HIP(launch(pc, true));
     }
     return RT_OK;
 }
@@ -384,12 +392,14 @@ rt_status rt_scene_create(rt_context* ctx, const rt_scene_desc* d, rt_scene** ou
         return o;
     };
     sc->off_sph = take(size_t(kSphStride) * sc->ns);
-    sc->off_sph_mat = take(size_t(kMatStride) * sc->ns);
     sc->off_pl = take(size_t(kPlStride) * sc->np);
-    sc->off_pl_mat = take(size_t(kMatStride) * sc->np);
     sc->off_tri = take(size_t(kTriStride) * sc->nt);
-    sc->off_tri_mat = take(size_t(kMatStride) * sc->nt);
     sc->off_lt = take(size_t(kLtStride) * sc->nl);
+    // one material table [spheres | planes | triangles]: a hit's material is one integer
+    // offset away (no pointer select, so global loads instead of flat ones)
+    sc->off_sph_mat = take(size_t(kMatStride) * (size_t(sc->ns) + sc->np + sc->nt));
+    sc->off_pl_mat = sc->off_sph_mat + size_t(kMatStride) * sc->ns;
+    sc->off_tri_mat = sc->off_pl_mat + size_t(kMatStride) * sc->np;
     std::vector<double> h(off + 2, 0.0);
 
     bool transparent = false;

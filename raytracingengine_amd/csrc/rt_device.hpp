@@ -133,6 +133,14 @@ __device__ __forceinline__ d3 tonemap_op(d3 c, int op) {
     }
     }
 }
+// The operators without libm calls (all but Reinhard-Jodie, op 4): lean kernels fuse only
+// these; a Jodie request selects the kernel variant that compiles tonemap_op in full.
+__device__ __forceinline__ d3 tonemap_op_nolog(d3 c, int op) {
+    switch (op) {
+    case 0: case 1: case 2: case 3: case 5: return tonemap_op(c, op);
+    default: return tonemap_op(c, 6);
+    }
+}
 // toColor (RaytracingEngine.cpp:113-121): clamp to [0,1], truncating cast of x*255.
 __device__ __forceinline__ void to_color(d3 v, uint8_t& r, uint8_t& g, uint8_t& b) {
     const d3 c = clamp3(v, 0.0, 1.0);

@@ -64,6 +64,10 @@ struct TraceParams {
 
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
                         hipStream_t stream);
+hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specular,
+                                hipStream_t stream);
+size_t packet_lds_bytes(int ns, int np, int nl);
+int packet_max_spheres();
 hipError_t launch_trace_rays(const TraceParams& p, int path, bool count, const double* rays,
                              size_t n, double* out, hipStream_t stream);
 hipError_t launch_intersect_rays(const TraceParams& p, const double* rays, size_t n, double* out,

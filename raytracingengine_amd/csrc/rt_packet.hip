@@ -1,0 +1,563 @@
+// rt_packet.hip — packet-culled FP64 trace kernel for scenes whose materials spawn no secondary
+// rays (every BASELINE synthetic config C2–C5): camera ray + shadow rays per pixel.
+//
+// Same per-ray arithmetic as the generic kernel (rt_trace_common.hpp), so results stay
+// bit-identical to the reference; what changes is WHICH spheres a ray is tested against:
+//
+//  * One wave = an 8×8 pixel tile.  Before each closest-hit search the wave bounds its rays —
+//    a direction cone around the camera for camera rays, a capsule from the ball of shadow-ray
+//    origins to the light for shadow rays — and each lane tests one sphere against that bound
+//    (ballot → a 64-bit candidate mask per 64 spheres, held in SGPRs).
+//  * The bound is conservative with a 1e-4 relative margin: a sphere outside it has, for every
+//    ray of the packet, an exact discriminant < 0 by far more than FP64 rounding can flip, so it
+//    can never be the closest hit nor produce a hit at all; candidates are visited in ascending
+//    index order so strict-'<' tie-breaking (HitInfo::isCloserThan, Shape.h:36) is unchanged.
+//    Spheres too far relative to their radius for that argument (|oc| > 1e5·r) are always kept.
+//  * Camera rays share their origin, so oc = cam − C and c = oc·oc − r² (Shape.h:73-77) are the
+//    same doubles for every camera ray: they are formed once per workgroup into LDS.
+//  * Shadow-ray marches (computeTransmittance, Scene.h:35-77) only move the origin along the
+//    segment towards the light, so one capsule mask serves the whole march.
+#include "rt_trace_common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace rtamd {
+
+constexpr int kPkW = 8;             // pixels per wave, x
+constexpr int kPkH = 8;             // pixels per wave, y
+constexpr int kWgWavesX = 2;        // waves per workgroup, x
+constexpr int kWgWavesY = 2;        // waves per workgroup, y
+constexpr double kCullRel = 1e-4;   // relative inflation of every culling radius
+constexpr double kCullCos = 1e-12;  // absolute slack on cosine comparisons
+constexpr double kFarRatio = 1e5;   // |oc|/r beyond which a sphere is never culled
+
+// Feature bits of a kernel variant: code for a feature the scene does not use is not compiled
+// in, which is what keeps the FP64 register budget (and so the occupancy) down.
+constexpr int kFeatSpec = 1;    // some opaque material has specular > 0: Blinn-Phong pow
+constexpr int kFeatArea = 2;    // build-defined area light
+constexpr int kFeatTris = 4;    // triangles / models
+constexpr int kFeatJodie = 8;   // Reinhard-Jodie fused tonemap (log/pow)
+constexpr int kFeatAll = 15;
+
+// ------------------------------------------------------------------ full-wave reductions
+// Every lane must be active.  IEEE add/min/max are commutative, so the xor butterfly leaves
+// the same value in all 64 lanes.
+__device__ __forceinline__ double wave_sum(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+struct PacketScene {
+    const double* sph;   // LDS: cx cy cz r²
+    const double* rad;   // LDS: radius (culling only)
+    const double* pre;   // LDS: camera-ray oc.xyz, oc·oc − r²
+    const double* pl;    // LDS: planes
+    const double* lt;    // LDS: point lights
+    const double* tri;   // HBM
+    const double* sph_mat;
+    const double* pl_mat;
+    const double* tri_mat;
+    int ns, np, nt, nl;
+};
+
+// Candidate masks: MAXC chunks of 64 spheres.  mask[c] is wave-uniform (a ballot result).
+template <int MAXC>
+struct Masks {
+    uint64_t m[MAXC];
+};
+
+// Camera-ray packet: origin `o` shared, directions within the cone (axis, cos_min).
+template <int MAXC>
+__device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 o, d3 axis,
+                                                 double cos_min) {
+    Masks<MAXC> M;
+    const int lane = threadIdx.x & 63;
+    const double sin_min = sqrt(fmax(0.0, 1.0 - cos_min * cos_min));
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int k = c * 64 + lane;
+        bool keep = false;
+        if (k < S.ns) {
+            const double* s = S.sph + kSphStride * k;
+            const double r = S.rad[k];
+            const d3 v = mk(s[0], s[1], s[2]) - o;
+            const double dv = length(v);
+            const double rr = r * (1.0 + kCullRel);
+            if (dv <= rr || dv > kFarRatio * r) {
+                keep = true;
+            } else {
+                const double sb = rr / dv;
+                const double cb = sqrt(fmax(0.0, 1.0 - sb * sb));
+                if (cb <= -cos_min) {
+                    keep = true;  // cone half-angle + sphere half-angle >= pi
+                } else {
+                    const double cos_bound = cos_min * cb - sin_min * sb;
+                    keep = dot(v, axis) / dv >= cos_bound - kCullCos;
+                }
+            }
+        }
+        M.m[c] = __ballot(keep);
+    }
+    return M;
+}
+
+// Shadow packet: origins inside ball (c, R), all rays end at a light inside ball (L, RL).
+template <int MAXC>
+__device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, double R, d3 L,
+                                                    double RL) {
+    Masks<MAXC> M;
+    const int lane = threadIdx.x & 63;
+    const d3 seg = L - c;
+    const double sl2 = dot(seg, seg);
+    const double Rc = fmax(R, RL);
+#pragma unroll
+    for (int ch = 0; ch < MAXC; ++ch) {
+        const int k = ch * 64 + lane;
+        bool keep = false;
+        if (k < S.ns) {
+            const double* s = S.sph + kSphStride * k;
+            const double r = S.rad[k];
+            const d3 v = mk(s[0], s[1], s[2]) - c;
+            const double t = sl2 > 0.0 ? fmin(1.0, fmax(0.0, dot(v, seg) / sl2)) : 0.0;
+            const double dist = length(v - seg * t);
+            keep = dist <= (r + Rc) * (1.0 + kCullRel) || length(v) + Rc > kFarRatio * r;
+        }
+        M.m[ch] = __ballot(keep);
+    }
+    return M;
+}
+
+// Sphere test of Shape.h:72-98 folded into the running closest (strict '<').
+__device__ __forceinline__ void sphere_candidate(double b, double disc, double two_a, int i,
+                                                 bool& found, double& best, int& kind, int& idx) {
+    if (disc < 0.0) return;
+    const double sq = sqrt(disc);
+    double t0 = (-b - sq) / two_a;
+    double t1 = (-b + sq) / two_a;
+    if (t0 > t1) {
+        const double tmp = t0;
+        t0 = t1;
+        t1 = tmp;
+    }
+    double t = t0;
+    if (t < 1e-6) {
+        t = t1;
+        if (t < 1e-6) return;
+    }
+    if (!found || t < best) {
+        found = true;
+        best = t;
+        kind = 1;
+        idx = i;
+    }
+}
+
+// Planes and triangles of IntersectClosest (never culled: few, and cheap).
+template <int FEAT>
+__device__ __forceinline__ void planes_tris(const PacketScene& S, d3 o, d3 d, bool& found,
+                                            double& best, int& kind, int& idx) {
+    for (int i = 0; i < S.np; ++i) {
+        const double* p = S.pl + kPlStride * i;
+        const d3 n = mk(p[3], p[4], p[5]);
+        const double denom = dot(n, d);
+        if (fabs(denom) > 1e-6) {
+            const double t = dot(mk(p[0], p[1], p[2]) - o, n) / denom;
+            if (t >= 0.0 && (!found || t < best)) {
+                found = true;
+                best = t;
+                kind = 2;
+                idx = i;
+            }
+        }
+    }
+    if (!(FEAT & kFeatTris)) return;
+    for (int i = 0; i < S.nt; ++i) {
+        const double* q = S.tri + kTriStride * i;
+        const d3 a0 = mk(q[0], q[1], q[2]);
+        const d3 e1 = mk(q[3], q[4], q[5]);
+        const d3 e2 = mk(q[6], q[7], q[8]);
+        const d3 hv = cross(d, e2);
+        const double det = dot(e1, hv);
+        if (det > -1e-6 && det < 1e-6) continue;
+        const double f = 1.0 / det;
+        const d3 sv = o - a0;
+        const double u = f * dot(sv, hv);
+        if (u < 0.0 || u > 1.0) continue;
+        const d3 qv = cross(sv, e1);
+        const double v = f * dot(d, qv);
+        if (v < 0.0 || u + v > 1.0) continue;
+        const double t = f * dot(e2, qv);
+        if (t > 1e-6 && (!found || t < best)) {
+            found = true;
+            best = t;
+            kind = 3;
+            idx = i;
+        }
+    }
+}
+
+// IntersectClosest for a camera ray (origin = camera) over the candidate spheres.
+template <int MAXC, int FEAT>
+__device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks<MAXC>& M,
+                                               int nchunks, d3 o, d3 d, Hit& h) {
+    bool found = false;
+    double best = 0.0;
+    int kind = 0, idx = -1;
+    const double a = dot(d, d);
+    const double two_a = 2.0 * a, four_a = 4.0 * a;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        if (c >= nchunks) break;
+        uint64_t m = M.m[c];
+        while (m) {
+            const int i = c * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            const double* q = S.pre + 4 * i;
+            const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
+            const double disc = b * b - four_a * q[3];
+            sphere_candidate(b, disc, two_a, i, found, best, kind, idx);
+        }
+    }
+    planes_tris<FEAT>(S, o, d, found, best, kind, idx);
+    h.t = best;
+    h.kind = kind;
+    h.idx = idx;
+    return found;
+}
+
+// IntersectClosest for an arbitrary ray over the candidate spheres.
+template <int MAXC, int FEAT>
+__device__ __forceinline__ bool closest_masked(const PacketScene& S, const Masks<MAXC>& M,
+                                               int nchunks, d3 o, d3 d, Hit& h) {
+    bool found = false;
+    double best = 0.0;
+    int kind = 0, idx = -1;
+    const double a = dot(d, d);
+    const double two_a = 2.0 * a, four_a = 4.0 * a;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        if (c >= nchunks) break;
+        uint64_t m = M.m[c];
+        while (m) {
+            const int i = c * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            const double* s = S.sph + kSphStride * i;
+            const d3 oc = o - mk(s[0], s[1], s[2]);
+            const double b = 2.0 * dot(oc, d);
+            const double cc = dot(oc, oc) - s[3];
+            const double disc = b * b - four_a * cc;
+            sphere_candidate(b, disc, two_a, i, found, best, kind, idx);
+        }
+    }
+    planes_tris<FEAT>(S, o, d, found, best, kind, idx);
+    h.t = best;
+    h.kind = kind;
+    h.idx = idx;
+    return found;
+}
+
+__device__ __forceinline__ const double* pk_material(const PacketScene& S, const Hit& h) {
+    // sph_mat heads the material table [spheres | planes | triangles]
+    const int base = h.kind == 1 ? 0 : (h.kind == 2 ? S.ns : S.ns + S.np);
+    return S.sph_mat + kMatStride * (base + h.idx);
+}
+
+__device__ __forceinline__ d3 pk_normal(const PacketScene& S, const Hit& h, d3 p) {
+    if (h.kind == 1) {
+        const double* s = S.sph + kSphStride * h.idx;
+        return unit(p - mk(s[0], s[1], s[2]));
+    }
+    if (h.kind == 2) {
+        const double* q = S.pl + kPlStride * h.idx;
+        return mk(q[3], q[4], q[5]);
+    }
+    const double* q = S.tri + kTriStride * h.idx;
+    return mk(q[9], q[10], q[11]);
+}
+
+// computeTransmittance (Scene.h:35-77) over the candidate spheres of the shadow packet.
+template <int MAXC, int FEAT>
+__device__ __forceinline__ double pk_transmittance(const PacketScene& S, const Masks<MAXC>& M,
+                                                   int nchunks, d3 o, d3 d, double max_dist,
+                                                   double bias) {
+    double T = 1.0, traveled = 0.0;
+    int safety = 64;
+    while (safety-- > 0 && T > 1e-4 && traveled < max_dist) {
+        Hit h;
+        if (!closest_masked<MAXC, FEAT>(S, M, nchunks, o, d, h)) break;
+        const double t = h.t;
+        if (t <= 0.0) {
+            o = o + d * bias;
+            traveled += bias;
+            continue;
+        }
+        if (t <= bias) {
+            o = (o + d * t) + d * bias;
+            traveled += t + bias;
+            continue;
+        }
+        if (traveled + t >= max_dist) break;
+        T *= sclamp(pk_material(S, h)[5], 0.0, 1.0);
+        o = (o + d * t) + d * bias;
+        traveled += t + bias;
+    }
+    return sclamp(T, 0.0, 1.0);
+}
+
+// One light of directLightning (Scene.h:86-124) for the whole wave: every lane calls it
+// (uniform control flow for the packet reductions); `active` lanes shade.
+template <int MAXC, int FEAT, bool COUNT>
+__device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P, d3 n, d3 view,
+                                         const Mat& m, d3 lpos, d3 E, d3 lcenter, double lrad,
+                                         double bias, int nchunks, d3& diff, d3& spec,
+                                         Counts& cnt) {
+    const d3 v = lpos - P;
+    const double dist = length(v);
+    const d3 L = sdiv(v, dist);
+    const double ndl = smax(0.0, dot(n, L));
+    const bool need = active && !(dist <= 0.0) && !(ndl <= 0.0) && !(dist <= bias);
+    const d3 so = P + n * bias;
+    // packet bound: ball around the origins of the lanes that cast this shadow ray
+    const double inf = __builtin_huge_val();
+    const double x0 = wave_min(need ? so.x : inf), x1 = wave_max(need ? so.x : -inf);
+    if (!(x0 <= x1)) return;  // no lane casts (uniform)
+    const double y0 = wave_min(need ? so.y : inf), y1 = wave_max(need ? so.y : -inf);
+    const double z0 = wave_min(need ? so.z : inf), z1 = wave_max(need ? so.z : -inf);
+    const d3 c = mk(0.5 * (x0 + x1), 0.5 * (y0 + y1), 0.5 * (z0 + z1));
+    const double R = wave_max(need ? length(so - c) : 0.0);
+    const Masks<MAXC> M = cull_capsule<MAXC>(S, c, R, lcenter, lrad);
+    if (!need) return;
+    if (COUNT) cnt.shadow++;
+    const double T = pk_transmittance<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
+    if (T <= bias) return;
+    const double inv_d2 = 1.0 / (dist * dist);
+    diff = diff + ((E * inv_d2) * ndl) * T;
+    if ((FEAT & kFeatSpec) && m.transparency <= 0.0 && m.specular > 0.0) {
+        const d3 H = unit(L + view);
+        const double ndh = smax(0.0, dot(n, H));
+        if (ndh > 0.0) {
+            const double sf = pow(ndh, m.shininess);
+            spec = spec + ((E * inv_d2) * sf) * T;
+        }
+    }
+}
+
+template <int MAXC, int FEAT, bool COUNT>
+__global__ __launch_bounds__(256) void packet_direct_kernel(TraceParams P) {
+    extern __shared__ double smem[];
+    const int tid = threadIdx.x;
+    const int ns = P.ns, np = P.np, nl = P.nl;
+    double* s_sph = smem;
+    double* s_rad = s_sph + kSphStride * ns;
+    double* s_pre = s_rad + ns;
+    double* s_pl = s_pre + 4 * ns;
+    double* s_lt = s_pl + kPlStride * np;
+    const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    for (int i = tid; i < kSphStride * ns; i += 256) s_sph[i] = P.sph[i];
+    for (int i = tid; i < ns; i += 256) {
+        const double* s = P.sph + kSphStride * i;
+        s_rad[i] = sqrt(s[3]);  // culling radius (sqrt(r²) ≈ r: only used with a margin)
+        // camera-ray constants of Sphere::Intersect (Shape.h:73,77)
+        const d3 oc = cam - mk(s[0], s[1], s[2]);
+        s_pre[4 * i + 0] = oc.x;
+        s_pre[4 * i + 1] = oc.y;
+        s_pre[4 * i + 2] = oc.z;
+        s_pre[4 * i + 3] = dot(oc, oc) - s[3];
+    }
+    for (int i = tid; i < kPlStride * np; i += 256) s_pl[i] = P.pl[i];
+    for (int i = tid; i < kLtStride * nl; i += 256) s_lt[i] = P.lt[i];
+    __syncthreads();
+
+    PacketScene S;
+    S.sph = s_sph;
+    S.rad = s_rad;
+    S.pre = s_pre;
+    S.pl = s_pl;
+    S.lt = s_lt;
+    S.tri = P.tri;
+    S.sph_mat = P.sph_mat;
+    S.pl_mat = P.pl_mat;
+    S.tri_mat = P.tri_mat;
+    S.ns = ns;
+    S.np = np;
+    S.nt = P.nt;
+    S.nl = nl;
+    const int nchunks = (ns + 63) / 64;
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const uint32_t x = blockIdx.x * (kPkW * kWgWavesX) + (wave % kWgWavesX) * kPkW + (lane % kPkW);
+    const uint32_t yl = blockIdx.y * (kPkH * kWgWavesY) + (wave / kWgWavesX) * kPkH + (lane / kPkW);
+    const bool valid = x < P.width && yl < P.rows;
+    // lanes past the image edge trace a clamped in-image ray: they take part in the packet
+    // reductions (a superset bound is still conservative) and write nothing.
+    const uint32_t xc = x < P.width ? x : P.width - 1;
+    const uint32_t y = P.row0 + (yl < P.rows ? yl : P.rows - 1);
+    const uint64_t pix = static_cast<uint64_t>(y) * P.width + xc;
+    const double bias = P.bias;
+    const bool area = P.al_samples > 0;
+    const d3 al_c = area ? (mk(P.al_corner[0], P.al_corner[1], P.al_corner[2]) +
+                            mk(P.al_u[0], P.al_u[1], P.al_u[2]) * 0.5) +
+                               mk(P.al_v[0], P.al_v[1], P.al_v[2]) * 0.5
+                         : mk(0.0, 0.0, 0.0);
+    const double al_r = area ? 0.5 * (length(mk(P.al_u[0], P.al_u[1], P.al_u[2])) +
+                                      length(mk(P.al_v[0], P.al_v[1], P.al_v[2])))
+                             : 0.0;
+    Counts cnt{0u, 0u};
+
+    d3 acc = mk(0.0, 0.0, 0.0);
+    int samples = 0;
+    for (int s = 0; s < P.aa; ++s) {
+        // Camera::getRay (Math.h:99-121)
+        double sx = static_cast<double>(xc) - static_cast<double>(P.width) / 2.0;
+        double sy = static_cast<double>(P.height) / 2.0 - static_cast<double>(y);
+        double jx = 0.0, jy = 0.0;
+        if (s > 0 && P.aa > 1) {
+            jx = u01(P.seed, pix, static_cast<uint32_t>(s), 0u);
+            jy = u01(P.seed, pix, static_cast<uint32_t>(s), 1u);
+        }
+        sx += jx;
+        sy += jy;
+        const d3 d = unit(mk(sx, sy, cam.z + P.focal) - cam);
+
+        d3 col;
+        if (P.max_rec <= 0) {
+            col = sky(d);  // TraceRay at depth >= maxRecursion (Scene.h:132-134)
+        } else {
+            if (COUNT && valid) cnt.trace++;
+            const d3 axis = unit(mk(wave_sum(d.x), wave_sum(d.y), wave_sum(d.z)));
+            const double cos_min = wave_min(dot(d, axis));
+            const Masks<MAXC> M = cull_cone<MAXC>(S, cam, axis, cos_min);
+            Hit h;
+            h.t = 0.0;
+            const bool hit = valid && closest_camera<MAXC, FEAT>(S, M, nchunks, cam, d, h);
+            // shading inputs (Scene.h:147-154); misses carry harmless placeholders
+            const d3 hp = cam + d * h.t;
+            const d3 gn = hit ? pk_normal(S, h, hp) : mk(0.0, 1.0, 0.0);
+            const Mat m = hit ? load_mat(pk_material(S, h)) : Mat{mk(0.0, 0.0, 0.0), 1.0, 0.0, 0.0, 1.0};
+            const d3 inc = unit(d);
+            const bool front = dot(gn, inc) < 0.0;
+            const d3 n0 = front ? gn : -gn;
+            const d3 view = -inc;
+            const d3 n = unit(n0);  // directLightning's own normalize (Scene.h:81)
+            d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
+            for (int l = 0; l < nl; ++l) {
+                const double* lp = S.lt + kLtStride * l;
+                const d3 L = mk(lp[0], lp[1], lp[2]);
+                pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, m, L, mk(lp[3], lp[4], lp[5]), L, 0.0,
+                                      bias, nchunks, diff, spec, cnt);
+            }
+            if ((FEAT & kFeatArea) && area) {
+                const uint32_t stream = 0x10000u + (static_cast<uint32_t>(s) << 6);
+                const double k = static_cast<double>(P.al_k);
+                const d3 corner = mk(P.al_corner[0], P.al_corner[1], P.al_corner[2]);
+                const d3 eu = mk(P.al_u[0], P.al_u[1], P.al_u[2]);
+                const d3 ev = mk(P.al_v[0], P.al_v[1], P.al_v[2]);
+                const d3 E = mk(P.al_E[0], P.al_E[1], P.al_E[2]);
+                for (int q = 0; q < P.al_samples; ++q) {
+                    const double r1 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q));
+                    const double r2 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q) + 1u);
+                    const double fu = (static_cast<double>(q % P.al_k) + r1) / k;
+                    const double fv = (static_cast<double>(q / P.al_k) + r2) / k;
+                    const d3 lpos = (corner + eu * fu) + ev * fv;
+                    pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, m, lpos, E, al_c, al_r, bias,
+                                          nchunks, diff, spec, cnt);
+                }
+            }
+            if (hit) {
+                const d3 local = hmul(m.color, diff) + spec * m.specular;
+                const double tr = sclamp(m.transparency, 0.0, 1.0);
+                d3 fin = mk(0.0, 0.0, 0.0);
+                if (tr < 1.0) fin = fin + local * (1.0 - tr);
+                col = fin;
+            } else {
+                col = sky(d);
+            }
+        }
+        acc = acc + col;
+        samples += 1;
+    }
+    if (valid) {
+        const d3 v = samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0);
+        const size_t o = static_cast<size_t>(yl) * P.width + x;
+        if (P.out64) {
+            P.out64[3 * o + 0] = v.x;
+            P.out64[3 * o + 1] = v.y;
+            P.out64[3 * o + 2] = v.z;
+        }
+        if (P.out32) {
+            P.out32[3 * o + 0] = static_cast<float>(v.x);
+            P.out32[3 * o + 1] = static_cast<float>(v.y);
+            P.out32[3 * o + 2] = static_cast<float>(v.z);
+        }
+        if (P.ldr) {
+            uint8_t r, g, b;
+            if constexpr ((FEAT & kFeatJodie) != 0) to_color(tonemap_op(v, P.tonemap), r, g, b);
+            else to_color(tonemap_op_nolog(v, P.tonemap), r, g, b);
+            P.ldr[3 * o + 0] = r;
+            P.ldr[3 * o + 1] = g;
+            P.ldr[3 * o + 2] = b;
+        }
+    }
+    if constexpr (COUNT) {
+        uint32_t t = cnt.trace, sh = cnt.shadow;
+        for (int off = 32; off > 0; off >>= 1) {
+            t += __shfl_xor(t, off, 64);
+            sh += __shfl_xor(sh, off, 64);
+        }
+        if (lane == 0) {
+            atomicAdd(P.counters + 0, static_cast<unsigned long long>(t));
+            atomicAdd(P.counters + 1, static_cast<unsigned long long>(sh));
+        }
+    }
+}
+
+size_t packet_lds_bytes(int ns, int np, int nl) {
+    return sizeof(double) * (static_cast<size_t>(kSphStride + 1 + 4) * ns +
+                             static_cast<size_t>(kPlStride) * np + static_cast<size_t>(kLtStride) * nl);
+}
+
+int packet_max_spheres() { return 16 * 64; }
+
+template <int MAXC, int FEAT>
+static void launch_packet_variant(const TraceParams& p, bool count, size_t lds, hipStream_t stream) {
+    const dim3 block(256);
+    const dim3 grid((p.width + kPkW * kWgWavesX - 1) / (kPkW * kWgWavesX),
+                    (p.rows + kPkH * kWgWavesY - 1) / (kPkH * kWgWavesY));
+    if (count) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, true>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false>), grid, block, lds, stream, p);
+}
+
+template <int MAXC>
+static void launch_packet_maxc(const TraceParams& p, bool count, size_t lds, int feat,
+                               hipStream_t stream) {
+    // three compiled feature sets: lean (the BASELINE C2-C4 shape), lean + area light (C5),
+    // and everything
+    if (feat == 0) launch_packet_variant<MAXC, 0>(p, count, lds, stream);
+    else if (feat == kFeatArea) launch_packet_variant<MAXC, kFeatArea>(p, count, lds, stream);
+    else launch_packet_variant<MAXC, kFeatAll>(p, count, lds, stream);
+}
+
+hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specular,
+                                hipStream_t stream) {
+    const size_t lds = packet_lds_bytes(p.ns, p.np, p.nl);
+    const int chunks = (p.ns + 63) / 64;
+    int feat = 0;
+    if (any_specular) feat |= kFeatSpec;
+    if (p.al_samples > 0) feat |= kFeatArea;
+    if (p.nt > 0) feat |= kFeatTris;
+    if (p.ldr && p.tonemap == 4) feat |= kFeatJodie;
+    if (chunks <= 1) launch_packet_maxc<1>(p, count, lds, feat, stream);
+    else if (chunks <= 4) launch_packet_maxc<4>(p, count, lds, feat, stream);
+    else launch_packet_maxc<16>(p, count, lds, feat, stream);
+    return hipGetLastError();
+}
+
+}  // namespace rtamd

@@ -13,402 +13,11 @@
 //     Triangle::Intersect :202-220) → directLightning :79-129 → computeTransmittance :35-77.
 // The recursion of TraceRay becomes an explicit stack: a linear chain (opaque mirrors) folded
 // back-to-front to keep the reference's rounding order, or a DFS stack for the refraction tree.
-#include "rt_device.hpp"
-#include "rt_internal.hpp"
+#include "rt_trace_common.hpp"
 
 #pragma clang fp contract(off)
 
 namespace rtamd {
-
-struct SceneView {
-    const double* sph;
-    const double* pl;
-    const double* lt;
-    const double* tri;
-    const double* sph_mat;
-    const double* pl_mat;
-    const double* tri_mat;
-    int ns, np, nt, nl;
-};
-
-struct Hit {
-    double t;
-    int kind;  // 1 sphere, 2 plane, 3 triangle
-    int idx;
-};
-
-struct Counts {
-    uint32_t trace;
-    uint32_t shadow;
-};
-
-// Scene::IntersectClosest: spheres, then planes, then triangles; a later candidate replaces
-// the current one only when strictly closer (HitInfo::isCloserThan, Shape.h:36).
-__device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) {
-    bool found = false;
-    double best = 0.0;
-    int kind = 0, idx = -1;
-    const double a = dot(d, d);       // Shape.h:75 (same value for every sphere)
-    const double two_a = 2.0 * a;     // Shape.h:85-86 denominator
-    const double four_a = 4.0 * a;    // Shape.h:79: (4.0 * a) * c
-    for (int i = 0; i < S.ns; ++i) {
-        const double* s = S.sph + kSphStride * i;
-        const d3 oc = o - mk(s[0], s[1], s[2]);
-        const double b = 2.0 * dot(oc, d);
-        const double c = dot(oc, oc) - s[3];
-        const double disc = b * b - four_a * c;
-        if (disc < 0.0) continue;
-        const double sq = sqrt(disc);
-        double t0 = (-b - sq) / two_a;
-        double t1 = (-b + sq) / two_a;
-        if (t0 > t1) {
-            const double tmp = t0;
-            t0 = t1;
-            t1 = tmp;
-        }
-        double t = t0;
-        if (t < 1e-6) {
-            t = t1;
-            if (t < 1e-6) continue;
-        }
-        if (!found || t < best) {
-            found = true;
-            best = t;
-            kind = 1;
-            idx = i;
-        }
-    }
-    for (int i = 0; i < S.np; ++i) {
-        const double* p = S.pl + kPlStride * i;
-        const d3 n = mk(p[3], p[4], p[5]);
-        const double denom = dot(n, d);
-        if (fabs(denom) > 1e-6) {
-            const d3 p0l0 = mk(p[0], p[1], p[2]) - o;
-            const double t = dot(p0l0, n) / denom;
-            if (t >= 0.0 && (!found || t < best)) {
-                found = true;
-                best = t;
-                kind = 2;
-                idx = i;
-            }
-        }
-    }
-    for (int i = 0; i < S.nt; ++i) {
-        const double* q = S.tri + kTriStride * i;
-        const d3 a0 = mk(q[0], q[1], q[2]);
-        const d3 e1 = mk(q[3], q[4], q[5]);
-        const d3 e2 = mk(q[6], q[7], q[8]);
-        const d3 hv = cross(d, e2);
-        const double det = dot(e1, hv);
-        if (det > -1e-6 && det < 1e-6) continue;
-        const double f = 1.0 / det;
-        const d3 sv = o - a0;
-        const double u = f * dot(sv, hv);
-        if (u < 0.0 || u > 1.0) continue;
-        const d3 qv = cross(sv, e1);
-        const double v = f * dot(d, qv);
-        if (v < 0.0 || u + v > 1.0) continue;
-        const double t = f * dot(e2, qv);
-        if (t > 1e-6 && (!found || t < best)) {
-            found = true;
-            best = t;
-            kind = 3;
-            idx = i;
-        }
-    }
-    h.t = best;
-    h.kind = kind;
-    h.idx = idx;
-    return found;
-}
-
-__device__ __forceinline__ const double* material_of(const SceneView& S, const Hit& h) {
-    return h.kind == 1 ? S.sph_mat + kMatStride * h.idx
-         : h.kind == 2 ? S.pl_mat + kMatStride * h.idx
-                       : S.tri_mat + kMatStride * h.idx;
-}
-
-// Geometric normal at the winner (Sphere::GetNormalAt Shape.h:100-102, Plane Shape.h:161-163,
-// Triangle::GetNormalAt Shape.h:222-227 precomputed on the host).
-__device__ __forceinline__ d3 normal_of(const SceneView& S, const Hit& h, d3 p) {
-    if (h.kind == 1) {
-        const double* s = S.sph + kSphStride * h.idx;
-        return unit(p - mk(s[0], s[1], s[2]));
-    }
-    if (h.kind == 2) {
-        const double* q = S.pl + kPlStride * h.idx;
-        return mk(q[3], q[4], q[5]);
-    }
-    const double* q = S.tri + kTriStride * h.idx;
-    return mk(q[9], q[10], q[11]);
-}
-
-// Scene::computeTransmittance (Scene.h:35-77): closest-hit march of up to 64 steps.
-__device__ __forceinline__ double transmittance(const SceneView& S, d3 o, d3 d, double max_dist,
-                                                double bias) {
-    double T = 1.0, traveled = 0.0;
-    int safety = 64;
-    while (safety-- > 0 && T > 1e-4 && traveled < max_dist) {
-        Hit h;
-        if (!closest(S, o, d, h)) break;
-        const double t = h.t;
-        if (t <= 0.0) {
-            o = o + d * bias;
-            traveled += bias;
-            continue;
-        }
-        if (t <= bias) {
-            o = (o + d * t) + d * bias;
-            traveled += t + bias;
-            continue;
-        }
-        if (traveled + t >= max_dist) break;
-        T *= sclamp(material_of(S, h)[5], 0.0, 1.0);
-        o = (o + d * t) + d * bias;
-        traveled += t + bias;
-    }
-    return sclamp(T, 0.0, 1.0);
-}
-
-struct Mat {
-    d3 color;
-    double shininess, specular, transparency, ior;
-};
-
-__device__ __forceinline__ Mat load_mat(const double* m) {
-    return Mat{mk(m[0], m[1], m[2]), m[3], m[4], m[5], m[6]};
-}
-
-// One iteration of directLightning's light loop (Scene.h:86-124).  E = color*intensity.
-template <bool COUNT>
-__device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 view, const Mat& m,
-                                           d3 lpos, d3 E, double bias, d3& diff, d3& spec,
-                                           Counts& cnt) {
-    const d3 v = lpos - P;
-    const double dist = length(v);
-    if (dist <= 0.0) return;
-    const d3 L = sdiv(v, dist);
-    const double ndl = smax(0.0, dot(n, L));
-    if (ndl <= 0.0) return;
-    if (dist <= bias) return;
-    if (COUNT) cnt.shadow++;
-    const double T = transmittance(S, P + n * bias, L, dist - bias, bias);
-    if (T <= bias) return;
-    const double inv_d2 = 1.0 / (dist * dist);
-    diff = diff + ((E * inv_d2) * ndl) * T;
-    if (m.transparency <= 0.0 && m.specular > 0.0) {
-        const d3 H = unit(L + view);
-        const double ndh = smax(0.0, dot(n, H));
-        if (ndh > 0.0) {
-            const double sf = pow(ndh, m.shininess);
-            spec = spec + ((E * inv_d2) * sf) * T;
-        }
-    }
-}
-
-// Scene::directLightning (Scene.h:79-129), plus the build-defined area-light samples.
-template <bool COUNT>
-__device__ __forceinline__ d3 direct(const SceneView& S, const TraceParams& P, d3 hp, d3 view,
-                                     d3 n_in, const Mat& m, uint64_t pix, uint32_t sample,
-                                     int depth, Counts& cnt) {
-    const double bias = P.bias;
-    const d3 n = unit(n_in);
-    d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
-    for (int i = 0; i < S.nl; ++i) {
-        const double* l = S.lt + kLtStride * i;
-        light_term<COUNT>(S, hp, n, view, m, mk(l[0], l[1], l[2]), mk(l[3], l[4], l[5]), bias,
-                          diff, spec, cnt);
-    }
-    if (P.al_samples > 0) {
-        const uint32_t stream = 0x10000u + (sample << 6) + static_cast<uint32_t>(depth);
-        const double k = static_cast<double>(P.al_k);
-        const d3 corner = mk(P.al_corner[0], P.al_corner[1], P.al_corner[2]);
-        const d3 eu = mk(P.al_u[0], P.al_u[1], P.al_u[2]);
-        const d3 ev = mk(P.al_v[0], P.al_v[1], P.al_v[2]);
-        const d3 E = mk(P.al_E[0], P.al_E[1], P.al_E[2]);
-        for (int s = 0; s < P.al_samples; ++s) {
-            const double r1 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(s));
-            const double r2 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(s) + 1u);
-            const double fu = (static_cast<double>(s % P.al_k) + r1) / k;
-            const double fv = (static_cast<double>(s / P.al_k) + r2) / k;
-            const d3 lp = (corner + eu * fu) + ev * fv;
-            light_term<COUNT>(S, hp, n, view, m, lp, E, bias, diff, spec, cnt);
-        }
-    }
-    return hmul(m.color, diff) + spec * m.specular;
-}
-
-// What one TraceRay invocation yields before its children are traced.
-struct Node {
-    d3 value;    // sky colour on a miss, else (0,0,0) + local*(1-tr) (Scene.h:175-179)
-    d3 ro, rd;   // reflection ray            (Scene.h:189-195)
-    d3 fo, fd;   // refraction ray            (Scene.h:181-187)
-    double rw;   // reflectiveness
-    double fw;   // transparency * (1 - fresnel)
-    bool hit, refl, refr;
-};
-
-template <bool TREE, bool COUNT>
-__device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, d3 o, d3 d,
-                                      uint64_t pix, uint32_t sample, int depth, Counts& cnt) {
-    Node nd;
-    nd.refl = false;
-    nd.refr = false;
-    if (COUNT) cnt.trace++;
-    Hit h;
-    if (!closest(S, o, d, h)) {
-        nd.hit = false;
-        nd.value = sky(d);
-        return nd;
-    }
-    nd.hit = true;
-    const double bias = P.bias;
-    const d3 hp = o + d * h.t;  // Rayon::pointAtDistance
-    const d3 gn = normal_of(S, h, hp);
-    const Mat m = load_mat(material_of(S, h));
-    const d3 inc = unit(d);
-    const bool front = dot(gn, inc) < 0.0;
-    const d3 n = front ? gn : -gn;
-    const d3 view = -inc;
-    const double tr = sclamp(m.transparency, 0.0, 1.0);
-    const d3 local = direct<COUNT>(S, P, hp, view, n, m, pix, sample, depth, cnt);
-    d3 fin = mk(0.0, 0.0, 0.0);
-    if (tr < 1.0) fin = fin + local * (1.0 - tr);
-    nd.value = fin;
-    double refl_w = m.specular;
-    if (TREE && tr > 0.0) {
-        // fresnel (Scene.h:26-28, 161-164); only consumed when tr > 0.
-        const double cos_t = smax(0.0, dot(n, view));
-        const double eta_t = m.ior;
-        const double r0 = (eta_t - 1.0) / (eta_t + 1.0);
-        const double f0 = r0 * r0;  // pow(x, 2.0)
-        double F = f0 + (1.0 - f0) * pow(1.0 - cos_t, 5.0);
-        const double eta = front ? (1.0 / eta_t) : (eta_t / 1.0);
-        d3 rd = refract(inc, n, eta);
-        if (length(rd) > bias) {
-            rd = unit(rd);
-            nd.refr = true;
-            nd.fd = rd;
-            nd.fo = hp + rd * (bias * 1e2);
-            nd.fw = tr * (1.0 - F);
-        } else {
-            F = 1.0;
-        }
-        refl_w = F;
-    }
-    if (refl_w > bias) {
-        const d3 R = unit(reflect(inc, n));
-        nd.refl = true;
-        nd.rd = R;
-        nd.ro = hp + R * bias;
-        nd.rw = refl_w;
-    }
-    return nd;
-}
-
-// TraceRay for scenes where no secondary ray can be spawned.
-template <bool COUNT>
-__device__ __forceinline__ d3 trace_direct(const SceneView& S, const TraceParams& P, d3 o, d3 d,
-                                           uint64_t pix, uint32_t sample, Counts& cnt) {
-    if (P.max_rec <= 0) return sky(d);
-    return shade<false, COUNT>(S, P, o, d, pix, sample, 0, cnt).value;
-}
-
-// TraceRay for opaque scenes: a linear reflection chain.  Levels are pushed front-to-back and
-// folded back-to-front, final_k = value_k + child_k * rw_k, the reference's rounding order.
-template <bool COUNT>
-__device__ __forceinline__ d3 trace_chain(const SceneView& S, const TraceParams& P, d3 o, d3 d,
-                                          uint64_t pix, uint32_t sample, Counts& cnt) {
-    d3 base[kMaxDepth];
-    double w[kMaxDepth];
-    int depth = 0;
-    d3 leaf;
-    while (true) {
-        if (depth >= P.max_rec) {
-            leaf = sky(d);
-            break;
-        }
-        const Node nd = shade<false, COUNT>(S, P, o, d, pix, sample, depth, cnt);
-        if (!nd.hit || !nd.refl) {
-            leaf = nd.value;
-            break;
-        }
-        base[depth] = nd.value;
-        w[depth] = nd.rw;
-        o = nd.ro;
-        d = nd.rd;
-        ++depth;
-    }
-    d3 acc = leaf;
-    for (int k = depth - 1; k >= 0; --k) acc = base[k] + acc * w[k];
-    return acc;
-}
-
-// TraceRay with transparency: depth-first walk of the refraction/reflection tree with an
-// explicit stack.  A frame waits first for its refraction child (added with weight fw), then
-// for its reflection child (weight rw), in the reference's accumulation order.
-template <bool COUNT>
-__device__ __forceinline__ d3 trace_tree(const SceneView& S, const TraceParams& P, d3 o, d3 d,
-                                         uint64_t pix, uint32_t sample, Counts& cnt) {
-    struct Frame {
-        d3 acc, ro, rd;
-        double rw, fw;
-        int phase;  // 1: waiting for the refraction child, 2: waiting for the reflection child
-        bool refl;
-    };
-    Frame st[kMaxDepth];
-    int sp = 0;
-    d3 val;
-    while (true) {
-        // descend from (o, d) at depth sp
-        if (sp >= P.max_rec) {
-            val = sky(d);
-        } else {
-            const Node nd = shade<true, COUNT>(S, P, o, d, pix, sample, sp, cnt);
-            if (nd.hit && (nd.refr || nd.refl)) {
-                Frame& f = st[sp];
-                f.acc = nd.value;
-                f.ro = nd.ro;
-                f.rd = nd.rd;
-                f.rw = nd.rw;
-                f.fw = nd.fw;
-                f.refl = nd.refl;
-                ++sp;
-                if (nd.refr) {
-                    f.phase = 1;
-                    o = nd.fo;
-                    d = nd.fd;
-                } else {
-                    f.phase = 2;
-                    o = nd.ro;
-                    d = nd.rd;
-                }
-                continue;
-            }
-            val = nd.value;
-        }
-        // ascend: fold `val` into the waiting frames
-        bool descend = false;
-        while (sp > 0) {
-            Frame& f = st[sp - 1];
-            if (f.phase == 1) {
-                f.acc = f.acc + val * f.fw;
-                if (f.refl) {
-                    f.phase = 2;
-                    o = f.ro;
-                    d = f.rd;
-                    descend = true;
-                    break;
-                }
-            } else {
-                f.acc = f.acc + val * f.rw;
-            }
-            val = f.acc;
-            --sp;
-        }
-        if (!descend) return val;
-    }
-}
 
 template <int PATH, bool COUNT, bool LDS>
 __global__ __launch_bounds__(kTileW * kTileH) void trace_kernel(TraceParams P) {
