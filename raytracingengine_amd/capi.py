@@ -13,7 +13,8 @@ import numpy as np
 from .scene import AREA_LIGHT_DTYPE, SceneData
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librtamd.so")
+# RTAMD_LIB overrides the library path (A/B builds in tools/); default: the in-tree build.
+LIB_PATH = os.environ.get("RTAMD_LIB", os.path.join(HERE, "librtamd.so"))
 
 RT_OK, RT_ERR_INVALID_ARG, RT_ERR_HIP, RT_ERR_OOM, RT_ERR_UNSUPPORTED, RT_ERR_NO_DEVICE = range(6)
 STATUS_NAMES = {0: "RT_OK", 1: "RT_ERR_INVALID_ARG", 2: "RT_ERR_HIP", 3: "RT_ERR_OOM",

@@ -35,9 +35,11 @@ __device__ __forceinline__ d3 cross(d3 a, d3 b) {
 }
 __device__ __forceinline__ double length(d3 a) { return sqrt(dot(a, a)); }
 // Vec3::normalize: zero vector below 1e-12, otherwise three true divisions.
+// x / 1.0 == x exactly (IEEE), so an already-unit vector skips its three divisions.
 __device__ __forceinline__ d3 unit(d3 a) {
     const double l = length(a);
     if (l <= 1e-12) return {0.0, 0.0, 0.0};
+    if (l == 1.0) return a;
     return sdiv(a, l);
 }
 // std::max / std::min / std::clamp with libstdc++'s comparison order (NaN handling).

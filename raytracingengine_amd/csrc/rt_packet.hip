@@ -2,19 +2,28 @@
 // rays (every BASELINE synthetic config C2–C5): camera ray + shadow rays per pixel.
 //
 // Same per-ray arithmetic as the generic kernel (rt_trace_common.hpp), so results stay
-// bit-identical to the reference; what changes is WHICH spheres a ray is tested against:
+// bit-identical to the reference; what changes is WHICH primitives a ray is tested against
+// and which divisions are skipped because their outcome is already decided:
 //
 //  * One wave = an 8×8 pixel tile.  Before each closest-hit search the wave bounds its rays —
 //    a direction cone around the camera for camera rays, a capsule from the ball of shadow-ray
 //    origins to the light for shadow rays — and each lane tests one sphere against that bound
-//    (ballot → a 64-bit candidate mask per 64 spheres, held in SGPRs).
-//  * The bound is conservative with a 1e-4 relative margin: a sphere outside it has, for every
-//    ray of the packet, an exact discriminant < 0 by far more than FP64 rounding can flip, so it
-//    can never be the closest hit nor produce a hit at all; candidates are visited in ascending
-//    index order so strict-'<' tie-breaking (HitInfo::isCloserThan, Shape.h:36) is unchanged.
-//    Spheres too far relative to their radius for that argument (|oc| > 1e5·r) are always kept.
-//  * Camera rays share their origin, so oc = cam − C and c = oc·oc − r² (Shape.h:73-77) are the
-//    same doubles for every camera ray: they are formed once per workgroup into LDS.
+//    (ballot → a 64-bit candidate mask per 64 spheres, held in SGPRs).  The bounds are reduced
+//    across the wave in FP32 with directed rounding (DPP row steps + readlane), so they only
+//    ever grow.
+//  * The per-sphere test is conservative with a 1e-4 relative radius margin: a sphere outside
+//    the bound has, for every ray of the packet, an exact discriminant < 0 by far more than
+//    FP64 rounding can flip, so it can never be hit.  Spheres whose |oc|/r exceeds 1e5 (where
+//    that argument would need a larger margin) are always kept.  Candidates are visited in
+//    ascending index order, so strict-'<' tie-breaking (Shape.h:36) is unchanged.
+//  * Camera rays share their origin: oc = cam − C, c = oc·oc − r² (Shape.h:73-77) and each
+//    plane's (p − cam)·n (Shape.h:152-153) are the same doubles for every camera ray and are
+//    formed once per workgroup into LDS.
+//  * A candidate's root (or plane t) is only divided out when it can still win: if
+//    numerator > best·denominator·(1+2⁻⁴⁰) the rounded quotient is provably ≥ best and the
+//    strict '<' would reject it anyway.  The far root is only formed when the near root is
+//    below the 1e-6 epsilon (t0 ≤ t1 holds exactly for 2a > 0, so the reference's swap never
+//    fires).
 //  * Shadow-ray marches (computeTransmittance, Scene.h:35-77) only move the origin along the
 //    segment towards the light, so one capsule mask serves the whole march.
 #include "rt_trace_common.hpp"
@@ -28,8 +37,9 @@ constexpr int kPkH = 8;             // pixels per wave, y
 constexpr int kWgWavesX = 2;        // waves per workgroup, x
 constexpr int kWgWavesY = 2;        // waves per workgroup, y
 constexpr double kCullRel = 1e-4;   // relative inflation of every culling radius
-constexpr double kCullCos = 1e-12;  // absolute slack on cosine comparisons
+constexpr double kCullSlack = 1e-9; // relative slack on the cone comparison
 constexpr double kFarRatio = 1e5;   // |oc|/r beyond which a sphere is never culled
+constexpr double kNoWin = 1.0 + 0x1.0p-40;  // "quotient provably >= best" factor
 
 // Feature bits of a kernel variant: code for a feature the scene does not use is not compiled
 // in, which is what keeps the FP64 register budget (and so the occupancy) down.
@@ -39,42 +49,70 @@ constexpr int kFeatTris = 4;    // triangles / models
 constexpr int kFeatJodie = 8;   // Reinhard-Jodie fused tonemap (log/pow)
 constexpr int kFeatAll = 15;
 
-// ------------------------------------------------------------------ full-wave reductions
-// Every lane must be active.  IEEE add/min/max are commutative, so the xor butterfly leaves
-// the same value in all 64 lanes.
-__device__ __forceinline__ double wave_sum(double v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// Waves per SIMD the lean variants are compiled for (4 = at most 128 VGPRs).
+#ifndef RT_PACKET_LEAN_WAVES
+#define RT_PACKET_LEAN_WAVES 4
+#endif
+
+// ------------------------------------------------------------------ wave reductions (FP32)
+// Every lane must be active.  Four DPP steps reduce each 16-lane row (quad xor-1, quad xor-2,
+// half-mirror, mirror: every lane of a row ends with the row's result), then the four row
+// values are read into SGPRs and combined in the same order in every lane.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
-__device__ __forceinline__ double wave_min(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
+__device__ __forceinline__ float lane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
-__device__ __forceinline__ double wave_max(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
+template <int OP>  // 0 min, 1 max
+__device__ __forceinline__ float wave_red(float v) {
+    auto op = [](float a, float b) { return OP == 0 ? fminf(a, b) : fmaxf(a, b); };
+    v = op(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = op(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = op(v, dpp<0x141>(v));  // row_half_mirror
+    v = op(v, dpp<0x140>(v));  // row_mirror
+    return op(op(lane_f(v, 0), lane_f(v, 16)), op(lane_f(v, 32), lane_f(v, 48)));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
 
 struct PacketScene {
     const double* sph;   // LDS: cx cy cz r²
     const double* rad;   // LDS: radius (culling only)
     const double* pre;   // LDS: camera-ray oc.xyz, oc·oc − r²
-    const double* pl;    // LDS: planes
+    const double* pl;    // LDS: planes (px py pz nx ny nz (p−cam)·n −)
     const double* lt;    // LDS: point lights
     const double* tri;   // HBM
-    const double* sph_mat;
-    const double* pl_mat;
-    const double* tri_mat;
+    const double* mat;   // HBM: material table [spheres | planes | triangles]
     int ns, np, nt, nl;
 };
 
-// Candidate masks: MAXC chunks of 64 spheres.  mask[c] is wave-uniform (a ballot result).
+// Candidate masks: MAXC chunks of 64 spheres.  m[c] is wave-uniform (a ballot result).
 template <int MAXC>
 struct Masks {
     uint64_t m[MAXC];
 };
 
+template <int MAXC>
+__device__ __forceinline__ Masks<MAXC> all_candidates(int ns) {
+    Masks<MAXC> M;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int left = ns - 64 * c;
+        M.m[c] = left >= 64 ? ~0ull : (left <= 0 ? 0ull : ((1ull << left) - 1ull));
+    }
+    return M;
+}
+
 // Camera-ray packet: origin `o` shared, directions within the cone (axis, cos_min).
+// Sphere (C, r) is kept iff angle(C−o, axis) ≤ θ + β, sin β = r'/|C−o| (r' = inflated r),
+// evaluated without divisions as  (C−o)·axis ≥ cosθ·√(|C−o|²−r'²) − sinθ·r'.
 template <int MAXC>
 __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 o, d3 axis,
                                                  double cos_min) {
@@ -89,19 +127,15 @@ __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 o, d3 
             const double* s = S.sph + kSphStride * k;
             const double r = S.rad[k];
             const d3 v = mk(s[0], s[1], s[2]) - o;
-            const double dv = length(v);
+            const double dv2 = dot(v, v);
             const double rr = r * (1.0 + kCullRel);
+            const double dv = sqrt(dv2);
             if (dv <= rr || dv > kFarRatio * r) {
                 keep = true;
             } else {
-                const double sb = rr / dv;
-                const double cb = sqrt(fmax(0.0, 1.0 - sb * sb));
-                if (cb <= -cos_min) {
-                    keep = true;  // cone half-angle + sphere half-angle >= pi
-                } else {
-                    const double cos_bound = cos_min * cb - sin_min * sb;
-                    keep = dot(v, axis) / dv >= cos_bound - kCullCos;
-                }
+                const double q = sqrt(dv2 - rr * rr);  // |C−o|·cos β
+                if (q <= -cos_min * dv) keep = true;    // θ + β ≥ π
+                else keep = dot(v, axis) >= cos_min * q - sin_min * rr - kCullSlack * dv;
             }
         }
         M.m[c] = __ballot(keep);
@@ -109,7 +143,8 @@ __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 o, d3 
     return M;
 }
 
-// Shadow packet: origins inside ball (c, R), all rays end at a light inside ball (L, RL).
+// Shadow packet: origins inside ball (c, R), every ray ends at a light inside ball (L, RL);
+// the segments lie in the capsule of radius max(R, RL) around [c, L].
 template <int MAXC>
 __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, double R, d3 L,
                                                     double RL) {
@@ -126,18 +161,48 @@ __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, 
             const double* s = S.sph + kSphStride * k;
             const double r = S.rad[k];
             const d3 v = mk(s[0], s[1], s[2]) - c;
-            const double t = sl2 > 0.0 ? fmin(1.0, fmax(0.0, dot(v, seg) / sl2)) : 0.0;
-            const double dist = length(v - seg * t);
-            keep = dist <= (r + Rc) * (1.0 + kCullRel) || length(v) + Rc > kFarRatio * r;
+            const double vs = dot(v, seg);
+            const double vv = dot(v, v);
+            // squared distance from C to the segment [c, L]
+            double d2;
+            if (vs <= 0.0 || !(sl2 > 0.0)) d2 = vv;
+            else if (vs >= sl2) d2 = dot(v - seg, v - seg);
+            else d2 = vv - (vs * vs) / sl2;
+            const double lim = (r + Rc) * (1.0 + kCullRel) + 1e-9 * sqrt(vv);
+            const double far = kFarRatio * r - Rc;
+            keep = d2 <= lim * lim || far <= 0.0 || vv > far * far;
         }
         M.m[ch] = __ballot(keep);
     }
     return M;
 }
 
-// Sphere test of Shape.h:72-98 folded into the running closest (strict '<').
-__device__ __forceinline__ void sphere_candidate(double b, double disc, double two_a, int i,
-                                                 bool& found, double& best, int& kind, int& idx) {
+// Root selection of Sphere::Intersect (Shape.h:84-97) folded into the running closest.
+// Requires two_a > 0 (then t0 ≤ t1 exactly); divisions are skipped when the candidate
+// provably cannot be strictly closer than `best`.
+__device__ __forceinline__ void sphere_roots(double b, double disc, double two_a, int i,
+                                             bool& found, double& best, int& kind, int& idx) {
+    if (disc < 0.0) return;
+    const double sq = sqrt(disc);
+    const double n0 = -b - sq;
+    if (found && n0 > (best * two_a) * kNoWin) return;  // t1 >= t0 >= best
+    double t = n0 / two_a;
+    if (t < 1e-6) {
+        t = (-b + sq) / two_a;
+        if (t < 1e-6) return;
+    }
+    if (!found || t < best) {
+        found = true;
+        best = t;
+        kind = 1;
+        idx = i;
+    }
+}
+
+// The reference's literal root selection, for degenerate directions (2a not > 0).
+__device__ __forceinline__ void sphere_roots_literal(double b, double disc, double two_a, int i,
+                                                     bool& found, double& best, int& kind,
+                                                     int& idx) {
     if (disc < 0.0) return;
     const double sq = sqrt(disc);
     double t0 = (-b - sq) / two_a;
@@ -160,24 +225,26 @@ __device__ __forceinline__ void sphere_candidate(double b, double disc, double t
     }
 }
 
-// Planes and triangles of IntersectClosest (never culled: few, and cheap).
-template <int FEAT>
-__device__ __forceinline__ void planes_tris(const PacketScene& S, d3 o, d3 d, bool& found,
-                                            double& best, int& kind, int& idx) {
-    for (int i = 0; i < S.np; ++i) {
-        const double* p = S.pl + kPlStride * i;
-        const d3 n = mk(p[3], p[4], p[5]);
-        const double denom = dot(n, d);
-        if (fabs(denom) > 1e-6) {
-            const double t = dot(mk(p[0], p[1], p[2]) - o, n) / denom;
-            if (t >= 0.0 && (!found || t < best)) {
-                found = true;
-                best = t;
-                kind = 2;
-                idx = i;
-            }
-        }
+// Plane::Intersect (Shape.h:149-159) given num = (p − o)·n and denom = n·d.
+__device__ __forceinline__ void plane_t(double num, double denom, int i, bool& found,
+                                        double& best, int& kind, int& idx) {
+    if (!(fabs(denom) > 1e-6)) return;
+    if (found) {  // skip the division when t = num/denom is provably >= best
+        const double lim = (best * denom) * kNoWin;
+        if (denom > 0.0 ? num > lim : num < lim) return;
     }
+    const double t = num / denom;
+    if (t >= 0.0 && (!found || t < best)) {
+        found = true;
+        best = t;
+        kind = 2;
+        idx = i;
+    }
+}
+
+template <int FEAT>
+__device__ __forceinline__ void triangles(const PacketScene& S, d3 o, d3 d, bool& found,
+                                          double& best, int& kind, int& idx) {
     if (!(FEAT & kFeatTris)) return;
     for (int i = 0; i < S.nt; ++i) {
         const double* q = S.tri + kTriStride * i;
@@ -204,7 +271,7 @@ __device__ __forceinline__ void planes_tris(const PacketScene& S, d3 o, d3 d, bo
     }
 }
 
-// IntersectClosest for a camera ray (origin = camera) over the candidate spheres.
+// IntersectClosest for a camera ray (origin = the camera) over the candidate spheres.
 template <int MAXC, int FEAT>
 __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks<MAXC>& M,
                                                int nchunks, d3 o, d3 d, Hit& h) {
@@ -213,6 +280,7 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
     int kind = 0, idx = -1;
     const double a = dot(d, d);
     const double two_a = 2.0 * a, four_a = 4.0 * a;
+    const bool regular = two_a > 0.0;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
         if (c >= nchunks) break;
@@ -223,10 +291,15 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
             const double* q = S.pre + 4 * i;
             const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
             const double disc = b * b - four_a * q[3];
-            sphere_candidate(b, disc, two_a, i, found, best, kind, idx);
+            if (regular) sphere_roots(b, disc, two_a, i, found, best, kind, idx);
+            else sphere_roots_literal(b, disc, two_a, i, found, best, kind, idx);
         }
     }
-    planes_tris<FEAT>(S, o, d, found, best, kind, idx);
+    for (int i = 0; i < S.np; ++i) {
+        const double* p = S.pl + kPlStride * i;
+        plane_t(p[6], dot(mk(p[3], p[4], p[5]), d), i, found, best, kind, idx);
+    }
+    triangles<FEAT>(S, o, d, found, best, kind, idx);
     h.t = best;
     h.kind = kind;
     h.idx = idx;
@@ -242,6 +315,7 @@ __device__ __forceinline__ bool closest_masked(const PacketScene& S, const Masks
     int kind = 0, idx = -1;
     const double a = dot(d, d);
     const double two_a = 2.0 * a, four_a = 4.0 * a;
+    const bool regular = two_a > 0.0;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
         if (c >= nchunks) break;
@@ -254,10 +328,16 @@ __device__ __forceinline__ bool closest_masked(const PacketScene& S, const Masks
             const double b = 2.0 * dot(oc, d);
             const double cc = dot(oc, oc) - s[3];
             const double disc = b * b - four_a * cc;
-            sphere_candidate(b, disc, two_a, i, found, best, kind, idx);
+            if (regular) sphere_roots(b, disc, two_a, i, found, best, kind, idx);
+            else sphere_roots_literal(b, disc, two_a, i, found, best, kind, idx);
         }
     }
-    planes_tris<FEAT>(S, o, d, found, best, kind, idx);
+    for (int i = 0; i < S.np; ++i) {
+        const double* p = S.pl + kPlStride * i;
+        const d3 n = mk(p[3], p[4], p[5]);
+        plane_t(dot(mk(p[0], p[1], p[2]) - o, n), dot(n, d), i, found, best, kind, idx);
+    }
+    triangles<FEAT>(S, o, d, found, best, kind, idx);
     h.t = best;
     h.kind = kind;
     h.idx = idx;
@@ -265,9 +345,8 @@ __device__ __forceinline__ bool closest_masked(const PacketScene& S, const Masks
 }
 
 __device__ __forceinline__ const double* pk_material(const PacketScene& S, const Hit& h) {
-    // sph_mat heads the material table [spheres | planes | triangles]
     const int base = h.kind == 1 ? 0 : (h.kind == 2 ? S.ns : S.ns + S.np);
-    return S.sph_mat + kMatStride * (base + h.idx);
+    return S.mat + kMatStride * (base + h.idx);
 }
 
 __device__ __forceinline__ d3 pk_normal(const PacketScene& S, const Hit& h, d3 p) {
@@ -316,42 +395,52 @@ __device__ __forceinline__ double pk_transmittance(const PacketScene& S, const M
 // (uniform control flow for the packet reductions); `active` lanes shade.
 template <int MAXC, int FEAT, bool COUNT>
 __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P, d3 n, d3 view,
-                                         const Mat& m, d3 lpos, d3 E, d3 lcenter, double lrad,
+                                         const Hit& h, d3 lpos, d3 E, d3 lcenter, double lrad,
                                          double bias, int nchunks, d3& diff, d3& spec,
                                          Counts& cnt) {
     const d3 v = lpos - P;
     const double dist = length(v);
-    const d3 L = sdiv(v, dist);
+    const bool reach = active && !(dist <= 0.0);
+    const d3 L = reach ? sdiv(v, dist) : mk(0.0, 0.0, 0.0);
     const double ndl = smax(0.0, dot(n, L));
-    const bool need = active && !(dist <= 0.0) && !(ndl <= 0.0) && !(dist <= bias);
+    const bool need = reach && !(ndl <= 0.0) && !(dist <= bias);
     const d3 so = P + n * bias;
-    // packet bound: ball around the origins of the lanes that cast this shadow ray
-    const double inf = __builtin_huge_val();
-    const double x0 = wave_min(need ? so.x : inf), x1 = wave_max(need ? so.x : -inf);
-    if (!(x0 <= x1)) return;  // no lane casts (uniform)
-    const double y0 = wave_min(need ? so.y : inf), y1 = wave_max(need ? so.y : -inf);
-    const double z0 = wave_min(need ? so.z : inf), z1 = wave_max(need ? so.z : -inf);
-    const d3 c = mk(0.5 * (x0 + x1), 0.5 * (y0 + y1), 0.5 * (z0 + z1));
-    const double R = wave_max(need ? length(so - c) : 0.0);
-    const Masks<MAXC> M = cull_capsule<MAXC>(S, c, R, lcenter, lrad);
+    // packet bound: FP32 AABB of the origins of the casting lanes (rounded outwards)
+    const float inf = __builtin_huge_valf();
+    const bool bad = need && !(isfinite(so.x) && isfinite(so.y) && isfinite(so.z));
+    const float x0 = wave_red<0>(need ? __double2float_rd(so.x) : inf);
+    if (!(x0 < inf)) return;  // no lane casts this shadow ray (uniform)
+    const float x1 = wave_red<1>(need ? __double2float_ru(so.x) : -inf);
+    const float y0 = wave_red<0>(need ? __double2float_rd(so.y) : inf);
+    const float y1 = wave_red<1>(need ? __double2float_ru(so.y) : -inf);
+    const float z0 = wave_red<0>(need ? __double2float_rd(so.z) : inf);
+    const float z1 = wave_red<1>(need ? __double2float_ru(so.z) : -inf);
+    const d3 c = mk(0.5 * (static_cast<double>(x0) + x1), 0.5 * (static_cast<double>(y0) + y1),
+                    0.5 * (static_cast<double>(z0) + z1));
+    const double R = wave_red<1>(need ? __double2float_ru(length(so - c)) : 0.0f);
+    const Masks<MAXC> M = __ballot(bad) ? all_candidates<MAXC>(S.ns)
+                                        : cull_capsule<MAXC>(S, c, R, lcenter, lrad);
     if (!need) return;
     if (COUNT) cnt.shadow++;
     const double T = pk_transmittance<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
     if (T <= bias) return;
     const double inv_d2 = 1.0 / (dist * dist);
     diff = diff + ((E * inv_d2) * ndl) * T;
-    if ((FEAT & kFeatSpec) && m.transparency <= 0.0 && m.specular > 0.0) {
-        const d3 H = unit(L + view);
-        const double ndh = smax(0.0, dot(n, H));
-        if (ndh > 0.0) {
-            const double sf = pow(ndh, m.shininess);
-            spec = spec + ((E * inv_d2) * sf) * T;
+    if constexpr ((FEAT & kFeatSpec) != 0) {
+        const double* m = pk_material(S, h);
+        if (m[5] <= 0.0 && m[4] > 0.0) {
+            const d3 H = unit(L + view);
+            const double ndh = smax(0.0, dot(n, H));
+            if (ndh > 0.0) {
+                const double sf = pow(ndh, m[3]);
+                spec = spec + ((E * inv_d2) * sf) * T;
+            }
         }
     }
 }
 
 template <int MAXC, int FEAT, bool COUNT>
-__global__ __launch_bounds__(256) void packet_direct_kernel(TraceParams P) {
+__global__ __launch_bounds__(256, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LEAN_WAVES : 1) void packet_direct_kernel(TraceParams P) {
     extern __shared__ double smem[];
     const int tid = threadIdx.x;
     const int ns = P.ns, np = P.np, nl = P.nl;
@@ -364,7 +453,7 @@ __global__ __launch_bounds__(256) void packet_direct_kernel(TraceParams P) {
     for (int i = tid; i < kSphStride * ns; i += 256) s_sph[i] = P.sph[i];
     for (int i = tid; i < ns; i += 256) {
         const double* s = P.sph + kSphStride * i;
-        s_rad[i] = sqrt(s[3]);  // culling radius (sqrt(r²) ≈ r: only used with a margin)
+        s_rad[i] = sqrt(s[3]);  // culling radius (only ever used with a margin)
         // camera-ray constants of Sphere::Intersect (Shape.h:73,77)
         const d3 oc = cam - mk(s[0], s[1], s[2]);
         s_pre[4 * i + 0] = oc.x;
@@ -372,7 +461,14 @@ __global__ __launch_bounds__(256) void packet_direct_kernel(TraceParams P) {
         s_pre[4 * i + 2] = oc.z;
         s_pre[4 * i + 3] = dot(oc, oc) - s[3];
     }
-    for (int i = tid; i < kPlStride * np; i += 256) s_pl[i] = P.pl[i];
+    for (int i = tid; i < np; i += 256) {
+        const double* p = P.pl + kPlStride * i;
+        double* o = s_pl + kPlStride * i;
+        for (int k = 0; k < 6; ++k) o[k] = p[k];
+        // camera-ray numerator of Plane::Intersect (Shape.h:152-153)
+        o[6] = dot(mk(p[0], p[1], p[2]) - cam, mk(p[3], p[4], p[5]));
+        o[7] = 0.0;
+    }
     for (int i = tid; i < kLtStride * nl; i += 256) s_lt[i] = P.lt[i];
     __syncthreads();
 
@@ -383,9 +479,7 @@ __global__ __launch_bounds__(256) void packet_direct_kernel(TraceParams P) {
     S.pl = s_pl;
     S.lt = s_lt;
     S.tri = P.tri;
-    S.sph_mat = P.sph_mat;
-    S.pl_mat = P.pl_mat;
-    S.tri_mat = P.tri_mat;
+    S.mat = P.sph_mat;
     S.ns = ns;
     S.np = np;
     S.nt = P.nt;
@@ -402,14 +496,14 @@ __global__ __launch_bounds__(256) void packet_direct_kernel(TraceParams P) {
     const uint32_t y = P.row0 + (yl < P.rows ? yl : P.rows - 1);
     const uint64_t pix = static_cast<uint64_t>(y) * P.width + xc;
     const double bias = P.bias;
-    const bool area = P.al_samples > 0;
-    const d3 al_c = area ? (mk(P.al_corner[0], P.al_corner[1], P.al_corner[2]) +
-                            mk(P.al_u[0], P.al_u[1], P.al_u[2]) * 0.5) +
-                               mk(P.al_v[0], P.al_v[1], P.al_v[2]) * 0.5
-                         : mk(0.0, 0.0, 0.0);
-    const double al_r = area ? 0.5 * (length(mk(P.al_u[0], P.al_u[1], P.al_u[2])) +
-                                      length(mk(P.al_v[0], P.al_v[1], P.al_v[2])))
-                             : 0.0;
+    d3 al_c = mk(0.0, 0.0, 0.0);
+    double al_r = 0.0;
+    if constexpr ((FEAT & kFeatArea) != 0) {
+        const d3 eu = mk(P.al_u[0], P.al_u[1], P.al_u[2]);
+        const d3 ev = mk(P.al_v[0], P.al_v[1], P.al_v[2]);
+        al_c = (mk(P.al_corner[0], P.al_corner[1], P.al_corner[2]) + eu * 0.5) + ev * 0.5;
+        al_r = (0.5 * (length(eu) + length(ev))) * (1.0 + kCullRel);
+    }
     Counts cnt{0u, 0u};
 
     d3 acc = mk(0.0, 0.0, 0.0);
@@ -432,16 +526,26 @@ __global__ __launch_bounds__(256) void packet_direct_kernel(TraceParams P) {
             col = sky(d);  // TraceRay at depth >= maxRecursion (Scene.h:132-134)
         } else {
             if (COUNT && valid) cnt.trace++;
-            const d3 axis = unit(mk(wave_sum(d.x), wave_sum(d.y), wave_sum(d.z)));
-            const double cos_min = wave_min(dot(d, axis));
-            const Masks<MAXC> M = cull_cone<MAXC>(S, cam, axis, cos_min);
+            // camera cone: FP32 axis, per-lane FP64 cosine rounded down, wave minimum
+            const float sxf = wave_sum(static_cast<float>(d.x));
+            const float syf = wave_sum(static_cast<float>(d.y));
+            const float szf = wave_sum(static_cast<float>(d.z));
+            const float il = 1.0f / sqrtf(sxf * sxf + syf * syf + szf * szf);
+            const d3 axis = mk(sxf * il, syf * il, szf * il);
+            const double cos_min =
+                static_cast<double>(wave_red<0>(__double2float_rd(dot(d, axis)))) - 1e-7;
+            const bool ok = isfinite(cos_min) && isfinite(axis.x) && isfinite(axis.y) &&
+                            isfinite(axis.z);
+            const Masks<MAXC> M = ok ? cull_cone<MAXC>(S, cam, axis, cos_min)
+                                     : all_candidates<MAXC>(ns);
             Hit h;
             h.t = 0.0;
+            h.kind = 0;
+            h.idx = 0;
             const bool hit = valid && closest_camera<MAXC, FEAT>(S, M, nchunks, cam, d, h);
             // shading inputs (Scene.h:147-154); misses carry harmless placeholders
             const d3 hp = cam + d * h.t;
             const d3 gn = hit ? pk_normal(S, h, hp) : mk(0.0, 1.0, 0.0);
-            const Mat m = hit ? load_mat(pk_material(S, h)) : Mat{mk(0.0, 0.0, 0.0), 1.0, 0.0, 0.0, 1.0};
             const d3 inc = unit(d);
             const bool front = dot(gn, inc) < 0.0;
             const d3 n0 = front ? gn : -gn;
@@ -451,29 +555,33 @@ __global__ __launch_bounds__(256) void packet_direct_kernel(TraceParams P) {
             for (int l = 0; l < nl; ++l) {
                 const double* lp = S.lt + kLtStride * l;
                 const d3 L = mk(lp[0], lp[1], lp[2]);
-                pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, m, L, mk(lp[3], lp[4], lp[5]), L, 0.0,
-                                      bias, nchunks, diff, spec, cnt);
+                pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, L, mk(lp[3], lp[4], lp[5]),
+                                            L, 0.0, bias, nchunks, diff, spec, cnt);
             }
-            if ((FEAT & kFeatArea) && area) {
-                const uint32_t stream = 0x10000u + (static_cast<uint32_t>(s) << 6);
-                const double k = static_cast<double>(P.al_k);
-                const d3 corner = mk(P.al_corner[0], P.al_corner[1], P.al_corner[2]);
-                const d3 eu = mk(P.al_u[0], P.al_u[1], P.al_u[2]);
-                const d3 ev = mk(P.al_v[0], P.al_v[1], P.al_v[2]);
-                const d3 E = mk(P.al_E[0], P.al_E[1], P.al_E[2]);
-                for (int q = 0; q < P.al_samples; ++q) {
-                    const double r1 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q));
-                    const double r2 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q) + 1u);
-                    const double fu = (static_cast<double>(q % P.al_k) + r1) / k;
-                    const double fv = (static_cast<double>(q / P.al_k) + r2) / k;
-                    const d3 lpos = (corner + eu * fu) + ev * fv;
-                    pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, m, lpos, E, al_c, al_r, bias,
-                                          nchunks, diff, spec, cnt);
+            if constexpr ((FEAT & kFeatArea) != 0) {
+                if (P.al_samples > 0) {
+                    const uint32_t stream = 0x10000u + (static_cast<uint32_t>(s) << 6);
+                    const double k = static_cast<double>(P.al_k);
+                    const d3 corner = mk(P.al_corner[0], P.al_corner[1], P.al_corner[2]);
+                    const d3 eu = mk(P.al_u[0], P.al_u[1], P.al_u[2]);
+                    const d3 ev = mk(P.al_v[0], P.al_v[1], P.al_v[2]);
+                    const d3 E = mk(P.al_E[0], P.al_E[1], P.al_E[2]);
+                    for (int q = 0; q < P.al_samples; ++q) {
+                        const double r1 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q));
+                        const double r2 =
+                            u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q) + 1u);
+                        const double fu = (static_cast<double>(q % P.al_k) + r1) / k;
+                        const double fv = (static_cast<double>(q / P.al_k) + r2) / k;
+                        const d3 lpos = (corner + eu * fu) + ev * fv;
+                        pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, lpos, E, al_c, al_r,
+                                                    bias, nchunks, diff, spec, cnt);
+                    }
                 }
             }
             if (hit) {
-                const d3 local = hmul(m.color, diff) + spec * m.specular;
-                const double tr = sclamp(m.transparency, 0.0, 1.0);
+                const double* m = pk_material(S, h);
+                const d3 local = hmul(mk(m[0], m[1], m[2]), diff) + spec * m[4];
+                const double tr = sclamp(m[5], 0.0, 1.0);
                 d3 fin = mk(0.0, 0.0, 0.0);
                 if (tr < 1.0) fin = fin + local * (1.0 - tr);
                 col = fin;
@@ -485,7 +593,9 @@ __global__ __launch_bounds__(256) void packet_direct_kernel(TraceParams P) {
         samples += 1;
     }
     if (valid) {
-        const d3 v = samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0);
+        // accumulated / samples (Scene.h:298-300); x / 1.0 == x, so AA=1 skips the division
+        const d3 v = samples == 1 ? acc
+                   : (samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0));
         const size_t o = static_cast<size_t>(yl) * P.width + x;
         if (P.out64) {
             P.out64[3 * o + 0] = v.x;

@@ -1,0 +1,20 @@
+"""Dev tool: render a config N times (for rocprofv3 counter collection)."""
+import sys
+sys.path.insert(0, '.')
+import torch
+from raytracingengine_amd import capi
+from raytracingengine_amd.configs import make_config
+name = sys.argv[1] if len(sys.argv) > 1 else "c2"
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+flags = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+ctx = capi.Context(0)
+s = torch.cuda.Stream(); ctx.set_stream(s.cuda_stream)
+sc = make_config(name)
+ds = ctx.scene(sc)
+W, H = sc.camera.width, sc.camera.height
+hdr = torch.empty(W * H * 3, dtype=torch.float32, device="cuda")
+ldr = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
+o = capi.default_opts(tonemap=1, flags=flags)
+for _ in range(reps):
+    ds.render_device(None, hdr.data_ptr(), ldr.data_ptr(), o)
+ctx.synchronize()
