@@ -74,12 +74,15 @@ __device__ __forceinline__ float wave_red(float v) {
     v = op(v, dpp<0x140>(v));  // row_mirror
     return op(op(lane_f(v, 0), lane_f(v, 16)), op(lane_f(v, 32), lane_f(v, 48)));
 }
-__device__ __forceinline__ float wave_sum(float v) {
-    v += dpp<0xB1>(v);
-    v += dpp<0x4E>(v);
-    v += dpp<0x141>(v);
-    v += dpp<0x140>(v);
-    return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+
+// Lane `l`'s double / vector, broadcast to every lane (exact: a bit copy via SGPRs).
+__device__ __forceinline__ double lane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ d3 lane_d3(d3 v, int l) {
+    return mk(lane_d(v.x, l), lane_d(v.y, l), lane_d(v.z, l));
 }
 
 struct PacketScene {
@@ -405,21 +408,16 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     const double ndl = smax(0.0, dot(n, L));
     const bool need = reach && !(ndl <= 0.0) && !(dist <= bias);
     const d3 so = P + n * bias;
-    // packet bound: FP32 AABB of the origins of the casting lanes (rounded outwards)
-    const float inf = __builtin_huge_valf();
+    // packet bound: a ball around the first casting lane's origin (exact), radius = the
+    // wave maximum of the distances, rounded up to FP32
+    const uint64_t casting = __ballot(need);
+    if (!casting) return;  // no lane casts this shadow ray (uniform)
     const bool bad = need && !(isfinite(so.x) && isfinite(so.y) && isfinite(so.z));
-    const float x0 = wave_red<0>(need ? __double2float_rd(so.x) : inf);
-    if (!(x0 < inf)) return;  // no lane casts this shadow ray (uniform)
-    const float x1 = wave_red<1>(need ? __double2float_ru(so.x) : -inf);
-    const float y0 = wave_red<0>(need ? __double2float_rd(so.y) : inf);
-    const float y1 = wave_red<1>(need ? __double2float_ru(so.y) : -inf);
-    const float z0 = wave_red<0>(need ? __double2float_rd(so.z) : inf);
-    const float z1 = wave_red<1>(need ? __double2float_ru(so.z) : -inf);
-    const d3 c = mk(0.5 * (static_cast<double>(x0) + x1), 0.5 * (static_cast<double>(y0) + y1),
-                    0.5 * (static_cast<double>(z0) + z1));
+    const d3 c = lane_d3(so, __builtin_ctzll(casting));
     const double R = wave_red<1>(need ? __double2float_ru(length(so - c)) : 0.0f);
-    const Masks<MAXC> M = __ballot(bad) ? all_candidates<MAXC>(S.ns)
-                                        : cull_capsule<MAXC>(S, c, R, lcenter, lrad);
+    const Masks<MAXC> M = __ballot(bad) || !isfinite(R)
+                              ? all_candidates<MAXC>(S.ns)
+                              : cull_capsule<MAXC>(S, c, R, lcenter, lrad);
     if (!need) return;
     if (COUNT) cnt.shadow++;
     const double T = pk_transmittance<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
@@ -526,16 +524,12 @@ __global__ __launch_bounds__(256, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LEAN_WAVE
             col = sky(d);  // TraceRay at depth >= maxRecursion (Scene.h:132-134)
         } else {
             if (COUNT && valid) cnt.trace++;
-            // camera cone: FP32 axis, per-lane FP64 cosine rounded down, wave minimum
-            const float sxf = wave_sum(static_cast<float>(d.x));
-            const float syf = wave_sum(static_cast<float>(d.y));
-            const float szf = wave_sum(static_cast<float>(d.z));
-            const float il = 1.0f / sqrtf(sxf * sxf + syf * syf + szf * szf);
-            const d3 axis = mk(sxf * il, syf * il, szf * il);
+            // camera cone: axis = the tile's centre-lane direction (exact copy), half-angle
+            // from the wave minimum of the per-lane cosines, rounded down to FP32
+            const d3 axis = lane_d3(d, (kPkH / 2) * kPkW + kPkW / 2);
             const double cos_min =
                 static_cast<double>(wave_red<0>(__double2float_rd(dot(d, axis)))) - 1e-7;
-            const bool ok = isfinite(cos_min) && isfinite(axis.x) && isfinite(axis.y) &&
-                            isfinite(axis.z);
+            const bool ok = isfinite(cos_min);
             const Masks<MAXC> M = ok ? cull_cone<MAXC>(S, cam, axis, cos_min)
                                      : all_candidates<MAXC>(ns);
             Hit h;
