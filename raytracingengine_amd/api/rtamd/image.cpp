@@ -1,12 +1,12 @@
 // rtamd/image.cpp — writePPM (host I/O boundary) and the device tonemap wrappers.
-#include "image.hpp"
+#include "rtamd/image.hpp"
 
 #include <cstdio>
 #include <iostream>
 #include <stdexcept>
 
 #include "rt_capi.h"
-#include "scene.hpp"
+#include "rtamd/scene.hpp"
 
 void writePPM(const std::string& filename, const std::vector<Color>& pixels, size_t width,
               size_t height) {

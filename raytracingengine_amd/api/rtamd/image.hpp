@@ -12,7 +12,7 @@
 #include <string>
 #include <vector>
 
-#include "math.hpp"
+#include "rtamd/math.hpp"
 
 void writePPM(const std::string& filename, const std::vector<Color>& pixels, size_t width,
               size_t height);

@@ -3,7 +3,7 @@
 // compatibility (the reference's shading does not call them either).
 #pragma once
 
-#include "math.hpp"
+#include "rtamd/math.hpp"
 
 // (build with -ffp-contract=off: no multiply-add fusion, as the reference's SSE2 build)
 

@@ -1,5 +1,5 @@
 // rtamd/scene.cpp — Scene methods over the C-ABI (see scene.hpp for the mapping).
-#include "scene.hpp"
+#include "rtamd/scene.hpp"
 
 #include <cstring>
 #include <map>

@@ -18,10 +18,10 @@
 #include <optional>
 #include <vector>
 
-#include "light.hpp"
-#include "math.hpp"
+#include "rtamd/light.hpp"
+#include "rtamd/math.hpp"
 #include "rt_capi.h"
-#include "shapes.hpp"
+#include "rtamd/shapes.hpp"
 
 namespace rtamd {
 struct SceneDevice;  // uploaded copy of a Scene on one device (scene.cpp)

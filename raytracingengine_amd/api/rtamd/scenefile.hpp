@@ -16,7 +16,7 @@
 #include <string>
 #include <vector>
 
-#include "scene.hpp"
+#include "rtamd/scene.hpp"
 
 namespace rtamd {
 

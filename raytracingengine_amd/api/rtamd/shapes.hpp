@@ -10,7 +10,7 @@
 #include <utility>
 #include <vector>
 
-#include "math.hpp"
+#include "rtamd/math.hpp"
 
 // (build with -ffp-contract=off: no multiply-add fusion, as the reference's SSE2 build)
 

@@ -99,6 +99,35 @@ def tonemap_inputs(rng):
     return px
 
 
+REFAPP_NAMES = ["simple", "reinhard_simple", "reinhard_extended", "reinhard_extended_luminance",
+                "reinhard_jodie", "uncharted2", "aces"]
+REFAPP_BLOCK = 20
+
+
+def ppm_blocks(path, block=REFAPP_BLOCK):
+    """Mean of every block×block pixel block of a P6 file written by writePPM."""
+    data = open(path, "rb").read()
+    header = b"P6\n1000 1000\n255\n"
+    assert data.startswith(header)
+    img = np.frombuffer(data[len(header):], np.uint8).reshape(1000, 1000, 3).astype(np.float64)
+    return img.reshape(1000 // block, block, 1000 // block, block, 3).mean(axis=(1, 3))
+
+
+def refapp_golden():
+    """Run the reference APPLICATION (its own main(), CPU renderer, AA=32) on tests/golden/box.obj
+    and keep 20x20 block means of its seven PPMs (the AA jitter is unseeded, so a statistical pin)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "refapp"], check=True)
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_app_cpu")
+    with tempfile.TemporaryDirectory() as td:
+        import shutil
+        shutil.copy(os.path.join(HERE, "box.obj"), td)
+        res = subprocess.run([exe], cwd=td, capture_output=True, text=True)
+        assert res.stdout.count("Image written") == 7, res.stdout
+        blocks = np.stack([ppm_blocks(os.path.join(td, f"{n}.ppm")) for n in REFAPP_NAMES])
+    np.savez_compressed(os.path.join(HERE, "refapp_blocks.npz"), blocks=blocks)
+    print("refapp blocks", blocks.shape)
+
+
 def main():
     if not po.ref_available():
         po.build()
@@ -184,4 +213,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--refapp" in sys.argv:
+        refapp_golden()
+    else:
+        main()
