@@ -49,6 +49,52 @@ def test_device_libm(ctx):
     assert np.all(np.abs(out[:, 3] - lg) <= np.spacing(np.abs(lg)))
 
 
+def _same_bits(a, b):
+    """Bitwise equality (signed zeros distinguished), any NaN equal to any NaN."""
+    nan = np.isnan(a) & np.isnan(b)
+    return np.array_equal(a.view(np.int64)[~nan], b.view(np.int64)[~nan]) and \
+        np.array_equal(np.isnan(a), np.isnan(b))
+
+
+def _edge_inputs():
+    rng = np.random.default_rng(11)
+    n = 60000
+    # log-uniform magnitudes over the whole binary64 range (denormals included), random signs
+    mag = lambda k: np.exp2(rng.uniform(-1074, 1023, k)) * rng.choice([-1.0, 1.0], k)
+    x, y = mag(n), mag(n)
+    # realistic operands: what the trace divides and takes roots of
+    x = np.concatenate([x, rng.uniform(-1e4, 1e4, n), rng.uniform(0, 1e6, n)])
+    y = np.concatenate([y, rng.uniform(-1e4, 1e4, n), rng.uniform(1e-6, 1e3, n)])
+    # near 1 (normalising unit vectors)
+    k = np.concatenate([np.arange(0, 5000), rng.integers(0, 1 << 26, 20000),
+                        (1 << 22) + np.arange(-64, 64)]).astype(np.int64)
+    one = np.float64(1.0).view(np.int64)
+    near = np.concatenate([(one + k).view(np.float64), (one - k).view(np.float64)])
+    x = np.concatenate([x, near])
+    y = np.concatenate([y, rng.uniform(0.5, 2.0, near.size)])
+    # scaling thresholds of the division/sqrt sequences and IEEE specials
+    edges = np.array([2.0 ** e * f for e in (-1074, -1023, -1022, -767, -700, -301, -300, -299,
+                                             299, 300, 301, 700, 1023)
+                      for f in (1.0, 1.0 - 2 ** -53, 1.0 + 2 ** -52, 1.5)])
+    special = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0, 5e-324, -5e-324,
+                        np.finfo(np.float64).max, np.finfo(np.float64).tiny])
+    ex = np.concatenate([edges, -edges, special])
+    gx, gy = np.meshgrid(ex, ex)
+    x = np.concatenate([x, gx.ravel()])
+    y = np.concatenate([y, gy.ravel()])
+    return x, y
+
+
+def test_device_div_sqrt_edge_cases(ctx):
+    """Device double division and sqrt give IEEE correctly rounded bits (numpy's) over the whole
+    binary64 range: zeros of both signs, denormals, infinities, NaN, near-1 operands."""
+    x, y = _edge_inputs()
+    with np.errstate(all="ignore"):
+        out = ctx.debug_f64_ops(x, y)
+        assert _same_bits(out[:, 0], x / y)
+        assert _same_bits(out[:, 1], np.sqrt(x))
+
+
 @pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4", "mirror", "glass", "mesh"])
 def test_small_scenes_vs_reference_golden(ctx, golden, name):
     sc = make_config(name, *SMALL)
