@@ -42,6 +42,10 @@ def parse_args(argv=None):
     ap.add_argument("--mode", choices=["frames", "tiled"], default="frames")
     ap.add_argument("--tonemap", default="reinhard_simple",
                     help="fused LDR operator, or 'none' (HDR only)")
+    ap.add_argument("--hdr", choices=["f64", "f32"], default="f64",
+                    help="HDR framebuffer type: f64 = the reference's std::vector<Vec3> (default)")
+    ap.add_argument("--event-every", type=int, default=10,
+                    help="bracket every n-th timed launch with HIP events (0: none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=6,
                     help="reference frames timed for cpu_baseline (first one is warm-up)")
@@ -123,16 +127,20 @@ def main(argv=None):
     else:  # contiguous row tile per rank
         row0, row1 = rank * H // world, (rank + 1) * H // world
     rows = row1 - row0
-    hdr = torch.empty(rows * W * 3, dtype=torch.float32, device="cuda")
+    hdr_dtype = torch.float64 if args.hdr == "f64" else torch.float32
+    hdr = torch.empty(rows * W * 3, dtype=hdr_dtype, device="cuda")
     ldr = torch.empty(rows * W * 3, dtype=torch.uint8, device="cuda") if tonemap >= 0 else None
+    def hdr_args():
+        return (hdr.data_ptr(), None) if args.hdr == "f64" else (None, hdr.data_ptr())
+
     full = None
     if args.mode == "tiled" and world > 1 and rank == 0:
-        full = [torch.empty(rows * W * 3, dtype=torch.float32, device="cuda") for _ in range(world)]
+        full = [torch.empty(rows * W * 3, dtype=hdr_dtype, device="cuda") for _ in range(world)]
 
     # ray counts of this rank's pixels (separate counting launch, not timed)
     with torch.cuda.stream(stream):
         ctx.reset_stats()
-        dscene.render_device(None, hdr.data_ptr(), None,
+        dscene.render_device(*hdr_args(), None,
                              capi.default_opts(tonemap=-1, row_begin=row0, row_end=row1,
                                                flags=capi.RT_FLAG_COUNT_RAYS))
         st = ctx.stats()
@@ -144,7 +152,7 @@ def main(argv=None):
                                    flags=capi.RT_FLAG_TIME_KERNEL)
 
     def step(o):
-        dscene.render_device(None, hdr.data_ptr(), ldr.data_ptr() if ldr is not None else None, o)
+        dscene.render_device(*hdr_args(), ldr.data_ptr() if ldr is not None else None, o)
         if args.mode == "tiled" and world > 1:
             with torch.cuda.stream(stream):
                 dist.gather(hdr, full if rank == 0 else None, dst=0)
@@ -154,16 +162,26 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(timed_opts)
+    ev0.record(stream)   # on the stream the trace kernel is launched on
+    for i in range(args.steps):
+        ev = args.event_every > 0 and i % args.event_every == 0
+        step(timed_opts if ev else opts)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    region_ms = ev0.elapsed_time(ev1) / args.steps
     elapsed = t1 - t0
     kst = ctx.stats()
-    kernel_ms = kst.kernel_ms / max(1, kst.launches)
+    # sampled per-launch events (every --event-every-th launch, bracketing the kernel alone)
+    sampled_ms = kst.kernel_ms / kst.launches if kst.launches else None
+    # frames mode: the kernel is the only work on the stream, so the region average is the
+    # launch duration including the back-to-back dispatch gap (agrees with rocprofv3 within a
+    # few %); tiled mode also runs the gather there, so the sampled launches are used.
+    kernel_ms = region_ms if args.mode == "frames" or sampled_ms is None else sampled_ms
 
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
@@ -185,7 +203,8 @@ def main(argv=None):
 
     if rank == 0:
         px = rows * W
-        bytes_per_launch = px * (12 + (3 if tonemap >= 0 else 0))  # float3 HDR + uint8 LDR
+        hdr_bytes = 24 if args.hdr == "f64" else 12
+        bytes_per_launch = px * (hdr_bytes + (3 if tonemap >= 0 else 0))  # Vec3 HDR + u8 LDR
         achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9
         traffic, traffic_src = load_traffic(args.config, args.mode)
         flops = rays_rank * alg_flops_per_ray(sc)
@@ -206,7 +225,7 @@ def main(argv=None):
             "config": {
                 "workload": f"{args.config}: {W}x{H}, {len(sc.spheres)} spheres, "
                             f"{len(sc.planes)} planes, {len(sc.lights)} point lights, AA=1, "
-                            f"float3 HDR + fused {args.tonemap} u8",
+                            f"{args.hdr} Vec3 HDR framebuffer + fused {args.tonemap} u8",
                 "global_batch": frames,
                 "resolution": [W, H],
                 "parallelism": (f"frames x{world}" if args.mode == "frames"
@@ -215,6 +234,7 @@ def main(argv=None):
             },
             "frames_per_sec": round(frames / elapsed, 3),
             "kernel_ms_per_launch": round(kernel_ms, 6),
+            "kernel_ms_sampled_events": round(sampled_ms, 6) if sampled_ms else None,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 2),

@@ -34,8 +34,15 @@ namespace rtamd {
 
 constexpr int kPkW = 8;             // pixels per wave, x
 constexpr int kPkH = 8;             // pixels per wave, y
-constexpr int kWgWavesX = 2;        // waves per workgroup, x
-constexpr int kWgWavesY = 2;        // waves per workgroup, y
+#ifndef RT_PK_WAVES_X
+#define RT_PK_WAVES_X 2
+#endif
+#ifndef RT_PK_WAVES_Y
+#define RT_PK_WAVES_Y 2
+#endif
+constexpr int kWgWavesX = RT_PK_WAVES_X;  // waves per workgroup, x
+constexpr int kWgWavesY = RT_PK_WAVES_Y;  // waves per workgroup, y
+constexpr int kWgThreads = 64 * kWgWavesX * kWgWavesY;
 constexpr double kCullRel = 1e-4;   // relative inflation of every culling radius
 constexpr double kCullSlack = 1e-9; // relative slack on the cone comparison
 constexpr double kFarRatio = 1e5;   // |oc|/r beyond which a sphere is never culled
@@ -438,7 +445,7 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
 }
 
 template <int MAXC, int FEAT, bool COUNT>
-__global__ __launch_bounds__(256, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LEAN_WAVES : 1) void packet_direct_kernel(TraceParams P) {
+__global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LEAN_WAVES : 1) void packet_direct_kernel(TraceParams P) {
     extern __shared__ double smem[];
     const int tid = threadIdx.x;
     const int ns = P.ns, np = P.np, nl = P.nl;
@@ -448,8 +455,8 @@ __global__ __launch_bounds__(256, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LEAN_WAVE
     double* s_pl = s_pre + 4 * ns;
     double* s_lt = s_pl + kPlStride * np;
     const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    for (int i = tid; i < kSphStride * ns; i += 256) s_sph[i] = P.sph[i];
-    for (int i = tid; i < ns; i += 256) {
+    for (int i = tid; i < kSphStride * ns; i += kWgThreads) s_sph[i] = P.sph[i];
+    for (int i = tid; i < ns; i += kWgThreads) {
         const double* s = P.sph + kSphStride * i;
         s_rad[i] = sqrt(s[3]);  // culling radius (only ever used with a margin)
         // camera-ray constants of Sphere::Intersect (Shape.h:73,77)
@@ -459,7 +466,7 @@ __global__ __launch_bounds__(256, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LEAN_WAVE
         s_pre[4 * i + 2] = oc.z;
         s_pre[4 * i + 3] = dot(oc, oc) - s[3];
     }
-    for (int i = tid; i < np; i += 256) {
+    for (int i = tid; i < np; i += kWgThreads) {
         const double* p = P.pl + kPlStride * i;
         double* o = s_pl + kPlStride * i;
         for (int k = 0; k < 6; ++k) o[k] = p[k];
@@ -467,7 +474,7 @@ __global__ __launch_bounds__(256, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LEAN_WAVE
         o[6] = dot(mk(p[0], p[1], p[2]) - cam, mk(p[3], p[4], p[5]));
         o[7] = 0.0;
     }
-    for (int i = tid; i < kLtStride * nl; i += 256) s_lt[i] = P.lt[i];
+    for (int i = tid; i < kLtStride * nl; i += kWgThreads) s_lt[i] = P.lt[i];
     __syncthreads();
 
     PacketScene S;
@@ -632,7 +639,7 @@ int packet_max_spheres() { return 16 * 64; }
 
 template <int MAXC, int FEAT>
 static void launch_packet_variant(const TraceParams& p, bool count, size_t lds, hipStream_t stream) {
-    const dim3 block(256);
+    const dim3 block(kWgThreads);
     const dim3 grid((p.width + kPkW * kWgWavesX - 1) / (kPkW * kWgWavesX),
                     (p.rows + kPkH * kWgWavesY - 1) / (kPkH * kWgWavesY));
     if (count) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, true>), grid, block, lds, stream, p);

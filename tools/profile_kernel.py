@@ -1,4 +1,5 @@
-"""Dev tool: render a config N times (for rocprofv3 counter collection)."""
+"""Dev tool: render a config N times with the bench's outputs (float64 Vec3 HDR framebuffer +
+fused tonemap bytes), for rocprofv3 kernel-trace / counter collection."""
 import sys
 sys.path.insert(0, '.')
 import torch
@@ -12,9 +13,9 @@ s = torch.cuda.Stream(); ctx.set_stream(s.cuda_stream)
 sc = make_config(name)
 ds = ctx.scene(sc)
 W, H = sc.camera.width, sc.camera.height
-hdr = torch.empty(W * H * 3, dtype=torch.float32, device="cuda")
+hdr = torch.empty(W * H * 3, dtype=torch.float64, device="cuda")
 ldr = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
 o = capi.default_opts(tonemap=1, flags=flags)
 for _ in range(reps):
-    ds.render_device(None, hdr.data_ptr(), ldr.data_ptr(), o)
+    ds.render_device(hdr.data_ptr(), None, ldr.data_ptr(), o)
 ctx.synchronize()
