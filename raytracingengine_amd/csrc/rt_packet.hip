@@ -120,32 +120,55 @@ __device__ __forceinline__ Masks<MAXC> all_candidates(int ns) {
     return M;
 }
 
-// Camera-ray packet: origin `o` shared, directions within the cone (axis, cos_min).
+// ------------------------------------------------------------------ packet culling (FP32)
+// The culls only decide which spheres a packet may skip, so they run in FP32 (half the FP64
+// issue cost, cheap sqrt) with every rounding error covered by explicit slack: each test keeps a
+// sphere unless the FP32 value clears the exact bound by more than kF32Slack times the
+// magnitudes involved (≥ 5× the worst-case FP32 error of the expression, derived per test
+// below).  Differences of scene coordinates are taken in FP64 first, so large coordinates do not
+// cost relative precision; NaN/inf anywhere keeps the sphere (every comparison is negated).
+constexpr float kF32Slack = 2e-5f;
+constexpr float kF32Up = 1.0f + 1e-6f;  // rounds a positive FP32 conversion up
+
+__device__ __forceinline__ float f32_up(double v) { return static_cast<float>(v) * kF32Up; }
+__device__ __forceinline__ float dot3f(float ax, float ay, float az, float bx, float by, float bz) {
+    return ax * bx + ay * by + az * bz;
+}
+
+// Camera-ray packet: origin `o` shared, directions within the cone (axis, cos_min), cos_min > 0.
 // Sphere (C, r) is kept iff angle(C−o, axis) ≤ θ + β, sin β = r'/|C−o| (r' = inflated r),
 // evaluated without divisions as  (C−o)·axis ≥ cosθ·√(|C−o|²−r'²) − sinθ·r'.
+// Error bound (d = |C−o|): |C−o|² and the dot product carry < 5e-7·d² and 3e-7·d; spheres with
+// d ≤ 1.01·r' are kept outright, so |C−o|²−r'² ≥ 0.0199·r'² and its square root is off by at
+// most 2.5e-6·d; total < 3e-6·d against a slack of 2e-5·d.
 template <int MAXC>
 __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 o, d3 axis,
                                                  double cos_min) {
     Masks<MAXC> M;
     const int lane = threadIdx.x & 63;
-    const double sin_min = sqrt(fmax(0.0, 1.0 - cos_min * cos_min));
+    const float cs = static_cast<float>(cos_min) * (1.0f - 1e-6f);  // rounded down (cs > 0)
+    const float sn = sqrtf(fmaxf(0.0f, 1.0f - cs * cs)) * (1.0f + 1e-5f);  // rounded up
+    const float ax = static_cast<float>(axis.x), ay = static_cast<float>(axis.y),
+                az = static_cast<float>(axis.z);
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
         const int k = c * 64 + lane;
         bool keep = false;
         if (k < S.ns) {
             const double* s = S.sph + kSphStride * k;
-            const double r = S.rad[k];
-            const d3 v = mk(s[0], s[1], s[2]) - o;
-            const double dv2 = dot(v, v);
-            const double rr = r * (1.0 + kCullRel);
-            const double dv = sqrt(dv2);
-            if (dv <= rr || dv > kFarRatio * r) {
+            const float r = f32_up(S.rad[k]);
+            const float vx = static_cast<float>(s[0] - o.x), vy = static_cast<float>(s[1] - o.y),
+                        vz = static_cast<float>(s[2] - o.z);
+            const float dv2 = dot3f(vx, vy, vz, vx, vy, vz);
+            const float rr = r * (1.0f + static_cast<float>(kCullRel));
+            const float dv = sqrtf(dv2);
+            if (!(dv > 1.01f * rr) || !(dv <= static_cast<float>(kFarRatio) * r)) {
                 keep = true;
             } else {
-                const double q = sqrt(dv2 - rr * rr);  // |C−o|·cos β
-                if (q <= -cos_min * dv) keep = true;    // θ + β ≥ π
-                else keep = dot(v, axis) >= cos_min * q - sin_min * rr - kCullSlack * dv;
+                const float q = sqrtf(dv2 - rr * rr);  // |C−o|·cos β
+                const float slack = kF32Slack * dv;
+                if (!(q > -cs * dv + slack)) keep = true;  // θ + β ≥ π
+                else keep = !(dot3f(vx, vy, vz, ax, ay, az) < cs * q - sn * rr - slack);
             }
         }
         M.m[c] = __ballot(keep);
@@ -154,33 +177,43 @@ __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 o, d3 
 }
 
 // Shadow packet: origins inside ball (c, R), every ray ends at a light inside ball (L, RL);
-// the segments lie in the capsule of radius max(R, RL) around [c, L].
+// the segments lie in the capsule of radius max(R, RL) around [c, L].  The squared distance
+// from C to the segment carries < 1.5e-6·(|C−c|² + |L−c|²) of FP32 error (any of the three
+// branches, including a branch chosen wrongly next to a boundary where they meet
+// continuously), against a slack of 2e-5·(|C−c|² + |L−c|²).
 template <int MAXC>
-__device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, double R, d3 L,
+__device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, float R, d3 L,
                                                     double RL) {
     Masks<MAXC> M;
     const int lane = threadIdx.x & 63;
-    const d3 seg = L - c;
-    const double sl2 = dot(seg, seg);
-    const double Rc = fmax(R, RL);
+    const float sx = static_cast<float>(L.x - c.x), sy = static_cast<float>(L.y - c.y),
+                sz = static_cast<float>(L.z - c.z);
+    const float sl2 = dot3f(sx, sy, sz, sx, sy, sz);
+    const float Rc = fmaxf(R, f32_up(RL));
 #pragma unroll
     for (int ch = 0; ch < MAXC; ++ch) {
         const int k = ch * 64 + lane;
         bool keep = false;
         if (k < S.ns) {
             const double* s = S.sph + kSphStride * k;
-            const double r = S.rad[k];
-            const d3 v = mk(s[0], s[1], s[2]) - c;
-            const double vs = dot(v, seg);
-            const double vv = dot(v, v);
-            // squared distance from C to the segment [c, L]
-            double d2;
-            if (vs <= 0.0 || !(sl2 > 0.0)) d2 = vv;
-            else if (vs >= sl2) d2 = dot(v - seg, v - seg);
-            else d2 = vv - (vs * vs) / sl2;
-            const double lim = (r + Rc) * (1.0 + kCullRel) + 1e-9 * sqrt(vv);
-            const double far = kFarRatio * r - Rc;
-            keep = d2 <= lim * lim || far <= 0.0 || vv > far * far;
+            const float r = f32_up(S.rad[k]);
+            const float vx = static_cast<float>(s[0] - c.x), vy = static_cast<float>(s[1] - c.y),
+                        vz = static_cast<float>(s[2] - c.z);
+            const float vs = dot3f(vx, vy, vz, sx, sy, sz);
+            const float vv = dot3f(vx, vy, vz, vx, vy, vz);
+            float d2;
+            if (!(vs > 0.0f) || !(sl2 > 0.0f)) {
+                d2 = vv;
+            } else if (!(vs < sl2)) {
+                const float wx = vx - sx, wy = vy - sy, wz = vz - sz;
+                d2 = dot3f(wx, wy, wz, wx, wy, wz);
+            } else {
+                d2 = vv - (vs * vs) / sl2;
+            }
+            const float lim = (r + Rc) * (1.0f + static_cast<float>(kCullRel));
+            const float far = static_cast<float>(kFarRatio) * r - Rc;
+            keep = !(d2 > lim * lim + kF32Slack * (vv + sl2)) || !(far > 0.0f) ||
+                   !(vv <= far * far);
         }
         M.m[ch] = __ballot(keep);
     }
@@ -421,7 +454,13 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     if (!casting) return;  // no lane casts this shadow ray (uniform)
     const bool bad = need && !(isfinite(so.x) && isfinite(so.y) && isfinite(so.z));
     const d3 c = lane_d3(so, __builtin_ctzll(casting));
-    const double R = wave_red<1>(need ? __double2float_ru(length(so - c)) : 0.0f);
+    float r_lane = 0.0f;
+    if (need) {  // |so − c| in FP32, rounded up (FP64 differences, 5e-7 relative FP32 error)
+        const float dx = static_cast<float>(so.x - c.x), dy = static_cast<float>(so.y - c.y),
+                    dz = static_cast<float>(so.z - c.z);
+        r_lane = sqrtf(dot3f(dx, dy, dz, dx, dy, dz)) * (1.0f + 1e-5f);
+    }
+    const float R = wave_red<1>(r_lane);
     const Masks<MAXC> M = __ballot(bad) || !isfinite(R)
                               ? all_candidates<MAXC>(S.ns)
                               : cull_capsule<MAXC>(S, c, R, lcenter, lrad);
@@ -536,7 +575,7 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
             const d3 axis = lane_d3(d, (kPkH / 2) * kPkW + kPkW / 2);
             const double cos_min =
                 static_cast<double>(wave_red<0>(__double2float_rd(dot(d, axis)))) - 1e-7;
-            const bool ok = isfinite(cos_min);
+            const bool ok = isfinite(cos_min) && cos_min > 0.0;  // cones narrower than 90°
             const Masks<MAXC> M = ok ? cull_cone<MAXC>(S, cam, axis, cos_min)
                                      : all_candidates<MAXC>(ns);
             Hit h;

@@ -1,0 +1,24 @@
+"""Dev tool: packet-kernel time only (no bit-exactness check), for ablation builds whose images
+are deliberately wrong.  RTAMD_LIB selects the build."""
+import sys, json
+sys.path.insert(0, '.')
+import torch
+from raytracingengine_amd import capi
+from raytracingengine_amd.configs import make_config
+ctx = capi.Context(0)
+s = torch.cuda.Stream(); ctx.set_stream(s.cuda_stream)
+for name in sys.argv[1:] or ["c2"]:
+    sc = make_config(name)
+    ds = ctx.scene(sc)
+    W, H = sc.camera.width, sc.camera.height
+    hdr = torch.empty(W * H * 3, dtype=torch.float64, device="cuda")
+    ldr = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
+    o = capi.default_opts(tonemap=1, flags=capi.RT_FLAG_TIME_KERNEL)
+    best = 1e9
+    for _ in range(4):
+        ctx.reset_stats()
+        for _ in range(20):
+            ds.render_device(hdr.data_ptr(), None, ldr.data_ptr(), o)
+        st = ctx.stats(); best = min(best, st.kernel_ms / st.launches)
+    print(name, "%.1f us" % (best * 1e3), flush=True)
+    ds.close()
