@@ -434,6 +434,82 @@ __device__ __forceinline__ double pk_transmittance(const PacketScene& S, const M
     return sclamp(T, 0.0, 1.0);
 }
 
+// Occlusion test for an all-opaque scene (the only kind this kernel renders: any material with
+// transparency > 0 goes to the tree kernel), where computeTransmittance (Scene.h:35-77) can only
+// return 1 (clear) or 0 (blocked): its first closest hit t* decides — t* in (bias, maxDist)
+// blocks, t* >= maxDist or no hit is clear, t* <= bias starts the march over near hits.  Each
+// candidate is classified with a FP32 square root and one shared FP64 reciprocal instead of the
+// reference's sqrt and division, with an explicit error bound Δ on every root; any root within
+// Δ of a threshold (1e-6, bias, maxDist), any near hit, or any value out of the fast ranges makes
+// the lane undecided, and undecided lanes run the exact march.  Returns 0 clear, 1 blocked,
+// 2 undecided.  The discriminant (and with it hit/miss) is the reference's FP64 expression.
+template <int MAXC, int FEAT>
+__device__ __forceinline__ int pk_occlusion(const PacketScene& S, const Masks<MAXC>& M,
+                                            int nchunks, d3 o, d3 d, double max_dist,
+                                            double bias) {
+    if constexpr ((FEAT & kFeatTris) != 0) return 2;
+    const double a = dot(d, d);
+    const double two_a = 2.0 * a, four_a = 4.0 * a;
+    if (!(two_a > 0.0)) return 2;
+    const double inv2a = 1.0 / two_a;
+    bool blocked = false, undecided = false;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        if (c >= nchunks) break;
+        uint64_t m = M.m[c];
+        while (m) {
+            const int i = c * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            const double* s = S.sph + kSphStride * i;
+            const d3 oc = o - mk(s[0], s[1], s[2]);
+            const double b = 2.0 * dot(oc, d);
+            const double cc = dot(oc, oc) - s[3];
+            const double disc = b * b - four_a * cc;
+            if (disc < 0.0) continue;  // miss, exactly as the reference decides it
+            if (!(disc == 0.0 || (disc > 1e-30 && disc < 1e30))) {
+                undecided = true;
+                continue;
+            }
+            // |sq − fl(√disc)| ≤ 5e-7·√disc (FP32 conversion + sqrtf), so both roots are within
+            // Δ = 2e-6·(|b| + sq)/2a of the reference's fl(fl(−b ∓ sq)/2a) (2× margin)
+            const double sq = static_cast<double>(sqrtf(static_cast<float>(disc)));
+            const double delta = 2e-6 * (fabs(b) + sq) * inv2a;
+            double t = (-b - sq) * inv2a;
+            if (!(t >= 1e-6 + delta)) {
+                if (!(t < 1e-6 - delta)) {
+                    undecided = true;
+                    continue;
+                }
+                t = (-b + sq) * inv2a;
+                if (t < 1e-6 - delta) continue;  // both roots behind: no hit
+                if (!(t >= 1e-6 + delta)) {
+                    undecided = true;
+                    continue;
+                }
+            }
+            if (t >= max_dist + delta) continue;              // beyond the light
+            if (t > bias + delta && t < max_dist - delta) blocked = true;
+            else undecided = true;                            // near hit or on a boundary
+        }
+    }
+    for (int i = 0; i < S.np; ++i) {
+        // Plane::Intersect (Shape.h:149-159): t = num / denom, decided without the division:
+        // with A = num·sign(denom), B = |denom|, t lies on the side of x that A lies of x·B
+        // (1e-9 relative margin ≫ the FP64 rounding of the quotient and the product)
+        const double* p = S.pl + kPlStride * i;
+        const d3 n = mk(p[3], p[4], p[5]);
+        const double denom = dot(n, d);
+        if (!(fabs(denom) > 1e-6)) continue;
+        const double num = dot(mk(p[0], p[1], p[2]) - o, n);
+        const double A = denom > 0.0 ? num : -num, B = fabs(denom);
+        if (A < -1e-300 * B) continue;                        // t < 0 (no underflow to −0)
+        if (A >= max_dist * B * (1.0 + 1e-9)) continue;       // beyond the light
+        if (A > bias * B * (1.0 + 1e-9) && A < max_dist * B * (1.0 - 1e-9)) blocked = true;
+        else undecided = true;
+    }
+    return undecided ? 2 : (blocked ? 1 : 0);
+}
+
 // One light of directLightning (Scene.h:86-124) for the whole wave: every lane calls it
 // (uniform control flow for the packet reductions); `active` lanes shade.
 template <int MAXC, int FEAT, bool COUNT>
@@ -466,7 +542,9 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
                               : cull_capsule<MAXC>(S, c, R, lcenter, lrad);
     if (!need) return;
     if (COUNT) cnt.shadow++;
-    const double T = pk_transmittance<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
+    const int occ = pk_occlusion<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
+    double T = occ == 1 ? 0.0 : 1.0;
+    if (occ == 2) T = pk_transmittance<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
     if (T <= bias) return;
     const double inv_d2 = 1.0 / (dist * dist);
     diff = diff + ((E * inv_d2) * ndl) * T;
