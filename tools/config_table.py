@@ -1,0 +1,53 @@
+"""Dev tool (GPU box): every config through the default path — kernel time by HIP events,
+Mrays/s (primary+shadow, exact counts from the counting pass) — next to the unmodified reference
+(oracle/_ref/ref_harness) timed on the host cores on a bounded sample: the same scene at a
+reduced resolution (same field of view) so each reference frame takes at most a few seconds.
+Writes one JSON object (list of rows) to stdout."""
+import json, os, sys
+sys.path.insert(0, '.')
+import torch
+from oracle import pyoracle as po
+from raytracingengine_amd import capi
+from raytracingengine_amd.configs import make_config
+
+CPU_SCALE = {"c1": 4, "c2": 4, "c3": 8, "c4": 16, "c5": 8, "mirror": 4, "glass": 4, "mesh": 4}
+threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+ctx = capi.Context(0)
+s = torch.cuda.Stream(); ctx.set_stream(s.cuda_stream)
+rows = []
+names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5", "mirror", "glass", "mesh"]
+for name in names:
+    sc = make_config(name)
+    ds = ctx.scene(sc)
+    W, H = sc.camera.width, sc.camera.height
+    hdr = torch.empty(W * H * 3, dtype=torch.float64, device="cuda")
+    ldr = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
+    a = ds.render(hdr64=False, stats=True)
+    rays = a["trace_rays"] + a["shadow_rays"]
+    o = capi.default_opts(tonemap=1, flags=capi.RT_FLAG_TIME_KERNEL)
+    best = 1e9
+    for _ in range(3):
+        ctx.reset_stats()
+        for _ in range(5):
+            ds.render_device(hdr.data_ptr(), None, ldr.data_ptr(), o)
+        st = ctx.stats(); best = min(best, st.kernel_ms / st.launches)
+    ds.close()
+    row = {"config": name, "resolution": [W, H], "spheres": len(sc.spheres),
+           "planes": len(sc.planes), "lights": len(sc.lights), "rays_per_frame": rays,
+           "gpu_ms_per_frame": round(best, 4), "gpu_mrays_s": round(rays / best / 1e3, 1)}
+    if po.ref_available():
+        k = CPU_SCALE[name]
+        small = make_config(name, W // k, H // k)
+        dss = ctx.scene(small)
+        b = dss.render(hdr64=False, stats=True)
+        dss.close()
+        srays = b["trace_rays"] + b["shadow_rays"]
+        _, ms, used = po.ref_render(small, repeat=3, threads=threads, want_image=False)
+        med = sorted(ms)[len(ms) // 2]
+        row.update({"cpu_sample": f"same scene at {W // k}x{H // k}, 3 frames, median",
+                    "cpu_threads": used, "cpu_ms_per_sample_frame": round(med, 2),
+                    "cpu_mrays_s": round(srays / med / 1e3, 2),
+                    "gpu_over_cpu": round(rays / best / (srays / med), 1)})
+    rows.append(row)
+    print(json.dumps(row), file=sys.stderr, flush=True)
+print(json.dumps(rows, indent=1))
