@@ -60,6 +60,7 @@ struct TraceParams {
     int32_t tonemap;
     int32_t _pad;
     unsigned long long* counters;  // [trace, shadow] — only written by the counting variant
+    const uint8_t* redo;  // generic kernels: when set, only pixels with a flagged sample run
 };
 
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,

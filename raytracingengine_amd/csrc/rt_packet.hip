@@ -44,7 +44,6 @@ constexpr int kWgWavesX = RT_PK_WAVES_X;  // waves per workgroup, x
 constexpr int kWgWavesY = RT_PK_WAVES_Y;  // waves per workgroup, y
 constexpr int kWgThreads = 64 * kWgWavesX * kWgWavesY;
 constexpr double kCullRel = 1e-4;   // relative inflation of every culling radius
-constexpr double kCullSlack = 1e-9; // relative slack on the cone comparison
 constexpr double kFarRatio = 1e5;   // |oc|/r beyond which a sphere is never culled
 constexpr double kNoWin = 1.0 + 0x1.0p-40;  // "quotient provably >= best" factor
 

@@ -22,38 +22,20 @@ namespace rtamd {
 template <int PATH, bool COUNT, bool LDS>
 __global__ __launch_bounds__(kTileW * kTileH) void trace_kernel(TraceParams P) {
     extern __shared__ double smem[];
-    SceneView S;
-    S.ns = P.ns;
-    S.np = P.np;
-    S.nt = P.nt;
-    S.nl = P.nl;
-    S.tri = P.tri;
-    S.sph_mat = P.sph_mat;
-    S.pl_mat = P.pl_mat;
-    S.tri_mat = P.tri_mat;
-    if constexpr (LDS) {
-        const int tid = threadIdx.y * kTileW + threadIdx.x;
-        constexpr int nthr = kTileW * kTileH;
-        double* s_sph = smem;
-        double* s_pl = s_sph + kSphStride * P.ns;
-        double* s_lt = s_pl + kPlStride * P.np;
-        for (int i = tid; i < kSphStride * P.ns; i += nthr) s_sph[i] = P.sph[i];
-        for (int i = tid; i < kPlStride * P.np; i += nthr) s_pl[i] = P.pl[i];
-        for (int i = tid; i < kLtStride * P.nl; i += nthr) s_lt[i] = P.lt[i];
-        __syncthreads();
-        S.sph = s_sph;
-        S.pl = s_pl;
-        S.lt = s_lt;
-    } else {
-        S.sph = P.sph;
-        S.pl = P.pl;
-        S.lt = P.lt;
-    }
-
+    const SceneView S = stage_scene<LDS>(P, smem, threadIdx.y * kTileW + threadIdx.x,
+                                         kTileW * kTileH);
     const uint32_t x = blockIdx.x * kTileW + threadIdx.x;
     const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
     Counts cnt{0u, 0u};
-    if (x < P.width && yl < P.rows) {
+    bool run = x < P.width && yl < P.rows;
+    if (run && P.redo) {
+        // fix-up pass of the wavefront renderer: only pixels with an incomplete sample tree
+        const size_t r0 = (static_cast<size_t>(yl) * P.width + x) * static_cast<size_t>(P.aa);
+        bool any = false;
+        for (int s = 0; s < P.aa; ++s) any = any || P.redo[r0 + s] != 0;
+        run = any;
+    }
+    if (run) {
         const uint32_t y = P.row0 + yl;
         const uint64_t pix = static_cast<uint64_t>(y) * P.width + x;
         const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
@@ -61,17 +43,7 @@ __global__ __launch_bounds__(kTileW * kTileH) void trace_kernel(TraceParams P) {
         d3 acc = mk(0.0, 0.0, 0.0);
         int samples = 0;
         for (int s = 0; s < P.aa; ++s) {
-            // Camera::getRay (Math.h:99-121); sample 0 is never jittered.
-            double sx = static_cast<double>(x) - static_cast<double>(P.width) / 2.0;
-            double sy = static_cast<double>(P.height) / 2.0 - static_cast<double>(y);
-            double jx = 0.0, jy = 0.0;
-            if (s > 0 && P.aa > 1) {
-                jx = u01(P.seed, pix, static_cast<uint32_t>(s), 0u);
-                jy = u01(P.seed, pix, static_cast<uint32_t>(s), 1u);
-            }
-            sx += jx;
-            sy += jy;
-            const d3 dir = unit(mk(sx, sy, cam.z + P.focal) - cam);
+            const d3 dir = camera_dir(P, cam, x, y, pix, s);
             d3 c;
             if constexpr (PATH == kPathDirect)
                 c = trace_direct<COUNT>(S, P, cam, dir, pix, static_cast<uint32_t>(s), cnt);
@@ -83,24 +55,7 @@ __global__ __launch_bounds__(kTileW * kTileH) void trace_kernel(TraceParams P) {
             samples += 1;
         }
         const d3 v = samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0);
-        const size_t o = static_cast<size_t>(yl) * P.width + x;
-        if (P.out64) {
-            P.out64[3 * o + 0] = v.x;
-            P.out64[3 * o + 1] = v.y;
-            P.out64[3 * o + 2] = v.z;
-        }
-        if (P.out32) {
-            P.out32[3 * o + 0] = static_cast<float>(v.x);
-            P.out32[3 * o + 1] = static_cast<float>(v.y);
-            P.out32[3 * o + 2] = static_cast<float>(v.z);
-        }
-        if (P.ldr) {
-            uint8_t r, g, b;
-            to_color(tonemap_op(v, P.tonemap), r, g, b);
-            P.ldr[3 * o + 0] = r;
-            P.ldr[3 * o + 1] = g;
-            P.ldr[3 * o + 2] = b;
-        }
+        store_pixel(P, static_cast<size_t>(yl) * P.width + x, v);
     }
     if constexpr (COUNT) {
         // wave-reduce the two counters, one 64-bit atomic per wave per counter

@@ -116,6 +116,76 @@ __device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) 
     return found;
 }
 
+// SceneView over the launch's scene; with LDS, sphere/plane/light records are staged into
+// `smem` by the whole workgroup first (every thread of the block must call this).
+template <bool LDS>
+__device__ __forceinline__ SceneView stage_scene(const TraceParams& P, double* smem, int tid,
+                                                 int nthr) {
+    SceneView S;
+    S.ns = P.ns;
+    S.np = P.np;
+    S.nt = P.nt;
+    S.nl = P.nl;
+    S.tri = P.tri;
+    S.sph_mat = P.sph_mat;
+    S.pl_mat = P.pl_mat;
+    S.tri_mat = P.tri_mat;
+    if constexpr (LDS) {
+        double* s_sph = smem;
+        double* s_pl = s_sph + kSphStride * P.ns;
+        double* s_lt = s_pl + kPlStride * P.np;
+        for (int i = tid; i < kSphStride * P.ns; i += nthr) s_sph[i] = P.sph[i];
+        for (int i = tid; i < kPlStride * P.np; i += nthr) s_pl[i] = P.pl[i];
+        for (int i = tid; i < kLtStride * P.nl; i += nthr) s_lt[i] = P.lt[i];
+        __syncthreads();
+        S.sph = s_sph;
+        S.pl = s_pl;
+        S.lt = s_lt;
+    } else {
+        S.sph = P.sph;
+        S.pl = P.pl;
+        S.lt = P.lt;
+    }
+    return S;
+}
+
+// GeneratePixelAt's result for row-local pixel offset `o`: float64 / float32 framebuffers and
+// the tonemapped bytes (Scene.h:298-300, RaytracingEngine.cpp:113-121).
+__device__ __forceinline__ void store_pixel(const TraceParams& P, size_t o, d3 v) {
+    if (P.out64) {
+        P.out64[3 * o + 0] = v.x;
+        P.out64[3 * o + 1] = v.y;
+        P.out64[3 * o + 2] = v.z;
+    }
+    if (P.out32) {
+        P.out32[3 * o + 0] = static_cast<float>(v.x);
+        P.out32[3 * o + 1] = static_cast<float>(v.y);
+        P.out32[3 * o + 2] = static_cast<float>(v.z);
+    }
+    if (P.ldr) {
+        uint8_t r, g, b;
+        to_color(tonemap_op(v, P.tonemap), r, g, b);
+        P.ldr[3 * o + 0] = r;
+        P.ldr[3 * o + 1] = g;
+        P.ldr[3 * o + 2] = b;
+    }
+}
+
+// Camera::getRay (Math.h:99-121) for pixel (x, y) and AA sample s; sample 0 is never jittered.
+__device__ __forceinline__ d3 camera_dir(const TraceParams& P, d3 cam, uint32_t x, uint32_t y,
+                                         uint64_t pix, int s) {
+    double sx = static_cast<double>(x) - static_cast<double>(P.width) / 2.0;
+    double sy = static_cast<double>(P.height) / 2.0 - static_cast<double>(y);
+    double jx = 0.0, jy = 0.0;
+    if (s > 0 && P.aa > 1) {
+        jx = u01(P.seed, pix, static_cast<uint32_t>(s), 0u);
+        jy = u01(P.seed, pix, static_cast<uint32_t>(s), 1u);
+    }
+    sx += jx;
+    sy += jy;
+    return unit(mk(sx, sy, cam.z + P.focal) - cam);
+}
+
 __device__ __forceinline__ const double* material_of(const SceneView& S, const Hit& h) {
     // sph_mat heads the material table [spheres | planes | triangles]
     const int base = h.kind == 1 ? 0 : (h.kind == 2 ? S.ns : S.ns + S.np);

@@ -1,0 +1,268 @@
+// rt_wavefront.hip — breadth-first ("wavefront") TraceRay for scenes with secondary rays.
+//
+// The reference recursion (Scene.h:131-198) spawns, per hit, a refraction ray (transparent
+// materials, Scene.h:181-187) and a reflection ray (Scene.h:189-195), so every pixel sample is a
+// binary tree of TraceRay calls.  Walking that tree per thread (rt_trace.hip, trace_tree) keeps
+// a 16-frame stack in scratch and leaves most lanes of a wave idle while the deepest tree of the
+// wave finishes.  Here the tree is processed level by level instead:
+//
+//   level kernel k   every ray of depth k is one thread: shade() (closest hit, directLightning
+//                    with its shadow rays — the same device code as the per-pixel kernels), the
+//                    node record (local value, refraction / reflection weights) is written, and
+//                    the child rays are appended to level k+1 with one atomic per wave;
+//   fold kernel k    deepest level first, value = (local + refraction_child·fw) +
+//                    reflection_child·rw — the reference's accumulation order (Scene.h:176-195);
+//   final kernel     the AA average of each pixel's root values, stored like GeneratePixelAt.
+//
+// Every ray is computed by the same instructions as in the per-pixel kernels and every node is
+// folded in the reference's order, so the image is bit-identical to them.  Node/ray records live
+// in one HBM arena of fixed capacity; a sample whose tree does not fit is flagged and its pixel
+// is re-rendered by the per-pixel kernel (P.redo) in the same stream, so capacity never changes
+// the result.  No host synchronisation: the ray count of each level lives in device memory and
+// the level kernels are persistent grids that loop over it.
+#include "rt_trace_common.hpp"
+#include "rt_wavefront.hpp"
+
+#pragma clang fp contract(off)
+
+namespace rtamd {
+
+namespace {
+
+constexpr int kWfThreads = 256;
+
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {  // set bits below this lane
+    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
+}
+
+// rays of level `level`: [base, base + n) in node ids, clamped to the arena
+__device__ __forceinline__ void level_range(const WfArena& A, int level, uint32_t& base,
+                                            uint32_t& n) {
+    if (level == 0) {
+        base = 0;
+        n = A.n0;
+        return;
+    }
+    base = A.ctl->base[level];
+    const uint32_t want = A.ctl->count[level];
+    n = base >= A.cap ? 0u : min(want, A.cap - base);
+}
+
+template <bool TREE, bool LDS>
+__global__ __launch_bounds__(kWfThreads) void wf_level_kernel(TraceParams P, WfArena A,
+                                                              int level) {
+    extern __shared__ double smem[];
+    const SceneView S = stage_scene<LDS>(P, smem, threadIdx.x, kWfThreads);
+    uint32_t base, n;
+    level_range(A, level, base, n);
+    const uint32_t next = base + n;  // first node id of level + 1
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.ctl->base[level + 1] = next;
+    const int lane = threadIdx.x & 63;
+    const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    const uint32_t aa = static_cast<uint32_t>(P.aa);
+    Counts cnt{0u, 0u};
+    // wave-uniform grid-stride loop: all 64 lanes run every iteration (ballots below)
+    for (uint32_t i0 = blockIdx.x * kWfThreads + (threadIdx.x & ~63u); i0 < n;
+         i0 += gridDim.x * kWfThreads) {
+        const uint32_t i = i0 + lane;
+        const bool active = i < n;
+        const uint32_t id = base + (active ? i : 0u);
+        uint32_t root;
+        d3 o, d;
+        if (level == 0) {
+            root = id;
+            const uint32_t pl = root / aa, s = root % aa;
+            const uint32_t x = pl % P.width, y = P.row0 + pl / P.width;
+            o = cam;
+            d = camera_dir(P, cam, x, y, static_cast<uint64_t>(y) * P.width + x,
+                           static_cast<int>(s));
+        } else {
+            const size_t r = id - A.n0;
+            root = A.root[r];
+            o = mk(A.ray[r], A.ray[A.cap_r + r], A.ray[2 * A.cap_r + r]);
+            d = mk(A.ray[3 * A.cap_r + r], A.ray[4 * A.cap_r + r], A.ray[5 * A.cap_r + r]);
+        }
+        const uint32_t pl = root / aa, sample = root % aa;
+        const uint64_t pix = static_cast<uint64_t>(P.row0 + pl / P.width) * P.width + pl % P.width;
+        Node nd;
+        nd.hit = false;
+        nd.refl = false;
+        nd.refr = false;
+        nd.fw = 0.0;
+        nd.rw = 0.0;
+        if (active) {
+            if (level >= P.max_rec) nd.value = sky(d);  // TraceRay at depth >= maxRecursion
+            else nd = shade<TREE, false>(S, P, o, d, pix, sample, level, cnt);
+        }
+        const bool want_f = active && TREE && nd.hit && nd.refr;
+        const bool want_r = active && nd.hit && nd.refl;
+        // one atomic per wave for all children of the wave
+        const uint64_t bf = __ballot(want_f), br = __ballot(want_r);
+        const uint32_t total = __builtin_popcountll(bf) + __builtin_popcountll(br);
+        uint32_t wbase = 0;
+        if (total) {
+            if (lane == 0) wbase = atomicAdd(&A.ctl->count[level + 1], total);
+            wbase = __shfl(wbase, 0, 64);
+        }
+        int32_t cf = -1, cr = -1;
+        bool lost = false;
+        if (want_f) {
+            const uint32_t cid = next + wbase + lane_prefix(bf);
+            if (cid < A.cap) {
+                const size_t r = cid - A.n0;
+                A.ray[r] = nd.fo.x;
+                A.ray[A.cap_r + r] = nd.fo.y;
+                A.ray[2 * A.cap_r + r] = nd.fo.z;
+                A.ray[3 * A.cap_r + r] = nd.fd.x;
+                A.ray[4 * A.cap_r + r] = nd.fd.y;
+                A.ray[5 * A.cap_r + r] = nd.fd.z;
+                A.root[r] = root;
+                cf = static_cast<int32_t>(cid);
+            } else {
+                lost = true;
+            }
+        }
+        if (want_r) {
+            const uint32_t cid =
+                next + wbase + __builtin_popcountll(bf) + lane_prefix(br);
+            if (cid < A.cap) {
+                const size_t r = cid - A.n0;
+                A.ray[r] = nd.ro.x;
+                A.ray[A.cap_r + r] = nd.ro.y;
+                A.ray[2 * A.cap_r + r] = nd.ro.z;
+                A.ray[3 * A.cap_r + r] = nd.rd.x;
+                A.ray[4 * A.cap_r + r] = nd.rd.y;
+                A.ray[5 * A.cap_r + r] = nd.rd.z;
+                A.root[r] = root;
+                cr = static_cast<int32_t>(cid);
+            } else {
+                lost = true;
+            }
+        }
+        if (lost) A.redo[root] = 1;  // the tree of this sample does not fit: per-pixel fix-up
+        if (active) {
+            A.val[id] = nd.value.x;
+            A.val[A.cap + id] = nd.value.y;
+            A.val[2 * A.cap + id] = nd.value.z;
+            A.fw[id] = nd.fw;
+            A.rw[id] = nd.rw;
+            A.child[id] = cf;
+            A.child[A.cap + id] = cr;
+        }
+    }
+}
+
+// value = (local + refraction·fw) + reflection·rw, deepest level first (Scene.h:176-195)
+__global__ __launch_bounds__(kWfThreads) void wf_fold_kernel(WfArena A, int level) {
+    uint32_t base, n;
+    level_range(A, level, base, n);
+    for (uint32_t i = blockIdx.x * kWfThreads + threadIdx.x; i < n; i += gridDim.x * kWfThreads) {
+        const uint32_t id = base + i;
+        const int32_t cf = A.child[id], cr = A.child[A.cap + id];
+        if (cf < 0 && cr < 0) continue;
+        d3 v = mk(A.val[id], A.val[A.cap + id], A.val[2 * A.cap + id]);
+        if (cf >= 0) v = v + mk(A.val[cf], A.val[A.cap + cf], A.val[2 * A.cap + cf]) * A.fw[id];
+        if (cr >= 0) v = v + mk(A.val[cr], A.val[A.cap + cr], A.val[2 * A.cap + cr]) * A.rw[id];
+        A.val[id] = v.x;
+        A.val[A.cap + id] = v.y;
+        A.val[2 * A.cap + id] = v.z;
+    }
+}
+
+// GeneratePixelAt (Scene.h:283-304): accumulated / samples, then the outputs
+__global__ __launch_bounds__(kWfThreads) void wf_final_kernel(TraceParams P, WfArena A) {
+    const size_t npx = static_cast<size_t>(P.rows) * P.width;
+    const size_t p = static_cast<size_t>(blockIdx.x) * kWfThreads + threadIdx.x;
+    if (p >= npx) return;
+    const size_t aa = P.aa > 0 ? static_cast<size_t>(P.aa) : 0;
+    for (size_t s = 0; s < aa; ++s)
+        if (A.redo[p * aa + s]) return;  // rendered by the fix-up pass
+    d3 acc = mk(0.0, 0.0, 0.0);
+    int samples = 0;
+    for (size_t s = 0; s < aa; ++s) {
+        const size_t id = p * aa + s;
+        acc = acc + mk(A.val[id], A.val[A.cap + id], A.val[2 * A.cap + id]);
+        samples += 1;
+    }
+    const d3 v = samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0);
+    store_pixel(P, p, v);
+}
+
+template <bool TREE, bool LDS>
+hipError_t launch_levels(const TraceParams& p, const WfArena& A, size_t lds_bytes,
+                         hipStream_t stream) {
+    const int max_level = p.max_rec > 0 ? p.max_rec : 0;
+    // level 0 exactly covers the roots; deeper levels are persistent grids over the arena
+    const uint32_t g0 = static_cast<uint32_t>((A.n0 + kWfThreads - 1) / kWfThreads);
+    const uint32_t gk = static_cast<uint32_t>(
+        std::min<size_t>(4096, (A.cap_r + kWfThreads - 1) / kWfThreads));
+    const size_t lds = LDS ? lds_bytes : 0;
+    if (g0 > 0)
+        hipLaunchKernelGGL((wf_level_kernel<TREE, LDS>), dim3(g0), dim3(kWfThreads), lds, stream,
+                           p, A, 0);
+    for (int k = 1; k <= max_level && gk > 0; ++k)
+        hipLaunchKernelGGL((wf_level_kernel<TREE, LDS>), dim3(gk), dim3(kWfThreads), lds, stream,
+                           p, A, k);
+    for (int k = max_level - 1; k >= 1 && gk > 0; --k)
+        hipLaunchKernelGGL(wf_fold_kernel, dim3(gk), dim3(kWfThreads), 0, stream, A, k);
+    if (g0 > 0 && max_level >= 1)
+        hipLaunchKernelGGL(wf_fold_kernel, dim3(g0), dim3(kWfThreads), 0, stream, A, 0);
+    const size_t npx = static_cast<size_t>(p.rows) * p.width;
+    if (npx > 0)
+        hipLaunchKernelGGL(wf_final_kernel, dim3(static_cast<uint32_t>((npx + kWfThreads - 1) /
+                                                                       kWfThreads)),
+                           dim3(kWfThreads), 0, stream, p, A);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t wf_arena_bytes(size_t n0, size_t cap) {
+    const size_t cap_r = cap - n0;
+    return sizeof(double) * (5 * cap + 6 * cap_r) + sizeof(int32_t) * 2 * cap +
+           sizeof(uint32_t) * cap_r + n0 + 64;
+}
+
+WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl) {
+    WfArena A;
+    A.n0 = static_cast<uint32_t>(n0);
+    A.cap = static_cast<uint32_t>(cap);
+    A.cap_r = static_cast<uint32_t>(cap - n0);
+    char* q = static_cast<char*>(mem);
+    A.val = reinterpret_cast<double*>(q);
+    q += sizeof(double) * 3 * cap;
+    A.fw = reinterpret_cast<double*>(q);
+    q += sizeof(double) * cap;
+    A.rw = reinterpret_cast<double*>(q);
+    q += sizeof(double) * cap;
+    A.ray = reinterpret_cast<double*>(q);
+    q += sizeof(double) * 6 * A.cap_r;
+    A.child = reinterpret_cast<int32_t*>(q);
+    q += sizeof(int32_t) * 2 * cap;
+    A.root = reinterpret_cast<uint32_t*>(q);
+    q += sizeof(uint32_t) * A.cap_r;
+    A.redo = reinterpret_cast<uint8_t*>(q);
+    A.ctl = ctl;
+    return A;
+}
+
+hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bool lds,
+                            size_t lds_bytes, hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(A.ctl, 0, sizeof(WfCtl), stream);
+    if (e == hipSuccess && A.n0 > 0) e = hipMemsetAsync(A.redo, 0, A.n0, stream);
+    if (e != hipSuccess) return e;
+    if (path == kPathTree)
+        e = lds ? launch_levels<true, true>(p, A, lds_bytes, stream)
+                : launch_levels<true, false>(p, A, lds_bytes, stream);
+    else
+        e = lds ? launch_levels<false, true>(p, A, lds_bytes, stream)
+                : launch_levels<false, false>(p, A, lds_bytes, stream);
+    if (e != hipSuccess) return e;
+    // fix-up: the per-pixel kernel for pixels whose sample trees overflowed the arena
+    TraceParams q = p;
+    q.redo = A.redo;
+    return launch_trace(q, path, false, lds, lds_bytes, stream);
+}
+
+}  // namespace rtamd

@@ -1,0 +1,37 @@
+// rt_wavefront.hpp — device arena of the breadth-first TraceRay (rt_wavefront.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rt_internal.hpp"
+
+namespace rtamd {
+
+// Per-level ray counts and first node ids, written by the level kernels (device memory).
+struct WfCtl {
+    uint32_t count[kMaxDepth + 2];
+    uint32_t base[kMaxDepth + 2];
+};
+
+// Node ids [0, n0) are the roots (pixel samples, row-local pixel * aa + sample); deeper nodes
+// are allocated level by level up to `cap`.  Structure-of-arrays, each component contiguous.
+struct WfArena {
+    double* val;      // 3 x cap: value of the node (local colour, then folded)
+    double* fw;       // cap: refraction weight transparency·(1 − F)
+    double* rw;       // cap: reflection weight
+    double* ray;      // 6 x cap_r: origin xyz, direction xyz of node n0 + r
+    int32_t* child;   // 2 x cap: refraction child id, reflection child id (−1: none)
+    uint32_t* root;   // cap_r: root id of node n0 + r
+    uint8_t* redo;    // n0: 1 = the tree of this root overflowed the arena
+    WfCtl* ctl;
+    uint32_t n0, cap, cap_r;
+};
+
+size_t wf_arena_bytes(size_t n0, size_t cap);
+WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl);
+hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bool lds,
+                            size_t lds_bytes, hipStream_t stream);
+
+}  // namespace rtamd

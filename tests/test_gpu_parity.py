@@ -289,3 +289,37 @@ def test_render_device_into_torch_buffers(ctx):
         ds.close()
     assert np.array_equal(h32.cpu().numpy().reshape(128, 256, 3), ref["hdr32"])
     assert np.array_equal(ldr.cpu().numpy().reshape(128, 256, 3), ref["ldr"])
+
+
+# ------------------------------------------------------------------ breadth-first TraceRay
+@pytest.mark.parametrize("name,aa,max_rec", [("glass", 1, 10), ("mirror", 1, 10), ("c1", 1, 10),
+                                             ("glass", 3, 6), ("mesh", 1, 10), ("glass", 1, 16)])
+def test_wavefront_equals_per_pixel_kernel(ctx, monkeypatch, name, aa, max_rec):
+    """Scenes with secondary rays render level by level (rt_wavefront.hip); the image must be
+    bit-identical to the per-pixel DFS kernel (RT_FLAG_GENERIC_KERNEL) — same rays, same fold
+    order — for the chain (mirror, c1) and the tree (glass) shapes, with AA and deep recursion."""
+    sc = make_config(name, 160, 90, aa=aa)
+    monkeypatch.setenv("RTAMD_WF_CHAIN", "1")  # chains are per-pixel by default
+    ds = ctx.scene(sc)
+    try:
+        a = ds.render(hdr64=True, tonemap=1, max_recursion=max_rec)
+        b = ds.render(hdr64=True, tonemap=1, max_recursion=max_rec,
+                      flags=capi.RT_FLAG_GENERIC_KERNEL)
+    finally:
+        ds.close()
+    assert np.array_equal(a["hdr64"], b["hdr64"], equal_nan=True)
+    assert np.array_equal(a["ldr"], b["ldr"])
+
+
+@pytest.mark.parametrize("mb", ["1", "2"])
+def test_wavefront_arena_overflow_falls_back_per_pixel(ctx, oracle, monkeypatch, mb):
+    """A tiny arena (RTAMD_WF_MB) overflows: the flagged samples are re-rendered by the
+    per-pixel kernel in the same stream, so the image is still the reference's."""
+    sc = make_config("glass", 320, 180)
+    monkeypatch.setenv("RTAMD_WF_MB", mb)
+    out = _render(ctx, sc, hdr64=True)
+    monkeypatch.delenv("RTAMD_WF_MB")
+    ref = _render(ctx, sc, hdr64=True, flags=capi.RT_FLAG_GENERIC_KERNEL)
+    assert np.array_equal(out["hdr64"], ref["hdr64"], equal_nan=True)
+    want, _, _ = oracle.render(sc, rows=(0, 20))
+    assert np.abs(out["hdr64"][:20] - want).max() <= POW_TOL
