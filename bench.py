@@ -42,6 +42,8 @@ def parse_args(argv=None):
     ap.add_argument("--mode", choices=["frames", "tiled"], default="frames")
     ap.add_argument("--tonemap", default="reinhard_simple",
                     help="fused LDR operator, or 'none' (HDR only)")
+    ap.add_argument("--row-block", type=int, default=16,
+                    help="tiled mode: rows per block of the block-cyclic split (0: contiguous)")
     ap.add_argument("--hdr", choices=["f64", "f32"], default="f64",
                     help="HDR framebuffer type: f64 = the reference's std::vector<Vec3> (default)")
     ap.add_argument("--event-every", type=int, default=10,
@@ -122,40 +124,59 @@ def main(argv=None):
     ctx.set_stream(stream.cuda_stream)
     dscene = ctx.scene(sc)
 
-    if args.mode == "frames":
-        row0, row1 = 0, H
-    else:  # contiguous row tile per rank
-        row0, row1 = rank * H // world, (rank + 1) * H // world
-    rows = row1 - row0
+    from raytracingengine_amd.distributed import plan_rows, render_opts_for, row_ranges
+    # frames: the whole image; tiled: this rank's rows of the one frame, dealt in
+    # blocks of --row-block rows round-robin (contiguous tiles of C3/C4 are 1.7x imbalanced)
+    block = args.row_block if args.mode == "tiled" else 0
+    nparts = world if args.mode == "tiled" else 1
+    plans = [row_ranges(r, nparts, H, block) for r in range(nparts)]
+    my_plan = plans[rank if args.mode == "tiled" else 0]
+    rows = plan_rows(my_plan)
+    max_rows = max(plan_rows(p) for p in plans)  # the gather moves equal-sized buffers
+
+    def make_opts(**kw):
+        return render_opts_for(my_plan, rank if args.mode == "tiled" else 0, nparts, H, block,
+                               **kw)
+
     hdr_dtype = torch.float64 if args.hdr == "f64" else torch.float32
-    hdr = torch.empty(rows * W * 3, dtype=hdr_dtype, device="cuda")
+    hdr = torch.zeros(max_rows * W * 3, dtype=hdr_dtype, device="cuda")
     ldr = torch.empty(rows * W * 3, dtype=torch.uint8, device="cuda") if tonemap >= 0 else None
     def hdr_args():
         return (hdr.data_ptr(), None) if args.hdr == "f64" else (None, hdr.data_ptr())
 
-    full = None
+    full = perm = None
     if args.mode == "tiled" and world > 1 and rank == 0:
-        full = [torch.empty(rows * W * 3, dtype=hdr_dtype, device="cuda") for _ in range(world)]
+        full = [torch.empty(max_rows * W * 3, dtype=hdr_dtype, device="cuda") for _ in range(world)]
+        # frame row y <- row perm[y] of the concatenated per-rank buffers
+        order = [0] * H
+        for r, plan in enumerate(plans):
+            k = r * max_rows
+            for a, b in plan:
+                for y in range(a, b):
+                    order[y] = k
+                    k += 1
+        perm = torch.tensor(order, dtype=torch.long, device="cuda")
 
     # ray counts of this rank's pixels (separate counting launch, not timed)
     with torch.cuda.stream(stream):
         ctx.reset_stats()
         dscene.render_device(*hdr_args(), None,
-                             capi.default_opts(tonemap=-1, row_begin=row0, row_end=row1,
-                                               flags=capi.RT_FLAG_COUNT_RAYS))
+                             make_opts(tonemap=-1, flags=capi.RT_FLAG_COUNT_RAYS))
         st = ctx.stats()
     rays_rank = st.trace_rays + st.shadow_rays
     ctx.reset_stats()
 
-    opts = capi.default_opts(tonemap=tonemap, row_begin=row0, row_end=row1)
-    timed_opts = capi.default_opts(tonemap=tonemap, row_begin=row0, row_end=row1,
-                                   flags=capi.RT_FLAG_TIME_KERNEL)
+    opts = make_opts(tonemap=tonemap)
+    timed_opts = make_opts(tonemap=tonemap, flags=capi.RT_FLAG_TIME_KERNEL)
 
     def step(o):
         dscene.render_device(*hdr_args(), ldr.data_ptr() if ldr is not None else None, o)
         if args.mode == "tiled" and world > 1:
             with torch.cuda.stream(stream):
                 dist.gather(hdr, full if rank == 0 else None, dst=0)
+                if rank == 0:  # assemble: rows back into image order (one device gather)
+                    frame = torch.cat(full).view(world * max_rows, W * 3).index_select(0, perm)
+                    del frame
 
     for _ in range(args.warmup):
         step(opts)
@@ -229,7 +250,8 @@ def main(argv=None):
                 "global_batch": frames,
                 "resolution": [W, H],
                 "parallelism": (f"frames x{world}" if args.mode == "frames"
-                                else f"row-tiles x{world} + RCCL gather"),
+                                else f"block-cyclic rows ({block}-row blocks) x{world} + "
+                                     f"RCCL gather"),
                 "rays_per_frame": rays_all if args.mode == "tiled" else rays_rank,
             },
             "frames_per_sec": round(frames / elapsed, 3),

@@ -149,7 +149,12 @@ typedef struct rt_render_opts {
     uint32_t row_begin;      /* render rows [row_begin, row_end) only (row tiles for        */
     uint32_t row_end;        /*  multi-GPU); row_end == 0 means the full image height       */
     int32_t flags;           /* RT_FLAG_* bits                                              */
-    int32_t _pad0;
+    /* Block-cyclic row sets (load-balanced multi-GPU frames).  With row_cycle > 1 the call
+     * renders the blocks of row_block rows starting at row_begin + k*row_cycle*row_block
+     * (k = 0, 1, ...), clipped to row_end, packed one after another in the outputs: rank r of
+     * n passes row_begin = r*row_block, row_cycle = n.  0 / 1: the contiguous range above. */
+    uint16_t row_block;
+    uint16_t row_cycle;
 } rt_render_opts;
 
 #define RT_FLAG_COUNT_RAYS 0x1   /* also run the ray-counting pass (fills rt_stats counts)   */

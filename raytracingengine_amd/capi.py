@@ -58,7 +58,7 @@ class RenderOpts(ctypes.Structure):
         ("max_recursion", ctypes.c_int32), ("tonemap", ctypes.c_int32),
         ("bias", ctypes.c_double), ("seed", ctypes.c_uint64),
         ("row_begin", ctypes.c_uint32), ("row_end", ctypes.c_uint32),
-        ("flags", ctypes.c_int32), ("_pad0", ctypes.c_int32),
+        ("flags", ctypes.c_int32), ("row_block", ctypes.c_uint16), ("row_cycle", ctypes.c_uint16),
     ]
 
 
@@ -120,6 +120,18 @@ def load_library(path: str = LIB_PATH):
 def _check(status: int):
     if status != RT_OK:
         raise RtError(status, _lib.rt_last_error().decode(errors="replace"))
+
+
+def rendered_rows(o: RenderOpts, height: int) -> int:
+    """Rows a render call produces (rt_capi.h rt_render_opts: a row range, or block-cyclic row
+    blocks when row_cycle > 1) — the height of the output buffers."""
+    r1 = min(o.row_end, height) if o.row_end else height
+    if r1 <= o.row_begin:
+        return 0
+    if o.row_cycle <= 1 or o.row_block == 0:
+        return r1 - o.row_begin
+    stride = o.row_block * o.row_cycle
+    return sum(min(o.row_block, r1 - b) for b in range(o.row_begin, r1, stride))
 
 
 def default_opts(**kw) -> RenderOpts:
@@ -235,9 +247,7 @@ class DeviceScene:
         o = opts if opts is not None else default_opts(tonemap=tonemap, **opt_kw)
         if opts is None:
             o.tonemap = tonemap
-        r0 = o.row_begin
-        r1 = o.row_end or cam.height
-        rows = r1 - r0 if r1 > r0 else 0
+        rows = rendered_rows(o, cam.height)
         out = {}
         a64 = np.empty((rows, cam.width, 3), np.float64) if hdr64 else None
         a32 = np.empty((rows, cam.width, 3), np.float32) if hdr32 else None

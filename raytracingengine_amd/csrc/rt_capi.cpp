@@ -105,6 +105,19 @@ struct rt_scene {
 
 namespace {
 
+// Rows a render call produces: [row_begin, row_end), or with row_cycle > 1 the row_block-row
+// blocks starting at row_begin + k*row_cycle*row_block inside it (rt_render_opts).
+uint32_t rendered_rows(const rt_render_opts& o, uint32_t height) {
+    const uint32_t r1 = o.row_end ? std::min(o.row_end, height) : height;
+    if (r1 <= o.row_begin) return 0;
+    if (o.row_cycle <= 1 || o.row_block == 0) return r1 - o.row_begin;
+    const uint64_t stride = static_cast<uint64_t>(o.row_block) * o.row_cycle;
+    uint64_t rows = 0;
+    for (uint64_t b = o.row_begin; b < r1; b += stride)
+        rows += std::min<uint64_t>(o.row_block, r1 - b);
+    return static_cast<uint32_t>(rows);
+}
+
 void pack_material(const rt_material& m, double* o) {
     o[0] = m.color[0];
     o[1] = m.color[1];
@@ -175,9 +188,11 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
         return fail(RT_ERR_INVALID_ARG, "row range [" + std::to_string(r0) + "," +
                                             std::to_string(r1) + ") invalid for height " +
                                             std::to_string(cam->height));
+    if (opts.row_cycle > 1 && opts.row_block == 0)
+        return fail(RT_ERR_INVALID_ARG, "row_cycle > 1 needs row_block >= 1");
     if (opts.tonemap < RT_TONEMAP_NONE || opts.tonemap >= RT_TONEMAP_COUNT)
         return fail(RT_ERR_INVALID_ARG, "tonemap operator out of range");
-    rows = r1 - r0;
+    rows = rendered_rows(opts, cam->height);
 
     const double* base = static_cast<const double*>(sc->buf.ptr);
     std::memset(&p, 0, sizeof p);
@@ -216,6 +231,10 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
     p.bias = opts.bias;
     p.seed = opts.seed;
     p.row0 = r0;
+    if (opts.row_cycle > 1) {
+        p.row_block = opts.row_block;
+        p.row_stride = static_cast<uint32_t>(opts.row_block) * opts.row_cycle;
+    }
     p.rows = rows;
     p.tonemap = opts.tonemap;
 
@@ -552,8 +571,7 @@ rt_status rt_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
     if (opts) o = *opts;
     else rt_render_opts_default(&o);
     if (stats) o.flags |= RT_FLAG_COUNT_RAYS;
-    const uint32_t r1 = o.row_end ? o.row_end : cam->height;
-    const uint32_t rows = r1 > o.row_begin ? r1 - o.row_begin : 0;
+    const uint32_t rows = rendered_rows(o, cam->height);
     const size_t npx = static_cast<size_t>(rows) * cam->width;
     if (h64) RT_HIP(ctx->out64.ensure(npx * 3 * sizeof(double)));
     if (h32) RT_HIP(ctx->out32.ensure(npx * 3 * sizeof(float)));

@@ -53,6 +53,7 @@ struct TraceParams {
     uint64_t seed;
     // tile
     uint32_t row0, rows;
+    uint32_t row_block, row_stride;  // block-cyclic rows (row_block 0: contiguous from row0)
     // outputs (device; any may be null)
     double* out64;
     float* out32;

@@ -614,7 +614,7 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
     // lanes past the image edge trace a clamped in-image ray: they take part in the packet
     // reductions (a superset bound is still conservative) and write nothing.
     const uint32_t xc = x < P.width ? x : P.width - 1;
-    const uint32_t y = P.row0 + (yl < P.rows ? yl : P.rows - 1);
+    const uint32_t y = image_row(P, yl < P.rows ? yl : P.rows - 1);
     const uint64_t pix = static_cast<uint64_t>(y) * P.width + xc;
     const double bias = P.bias;
     d3 al_c = mk(0.0, 0.0, 0.0);

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(kTileW * kTileH) void trace_kernel(TraceParams P) {
         run = any;
     }
     if (run) {
-        const uint32_t y = P.row0 + yl;
+        const uint32_t y = image_row(P, yl);
         const uint64_t pix = static_cast<uint64_t>(y) * P.width + x;
         const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
         // GeneratePixelAt (Scene.h:283-304)

@@ -116,6 +116,12 @@ __device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) 
     return found;
 }
 
+// Image row of the launch's row-local row yl (contiguous, or block-cyclic for multi-GPU).
+__device__ __forceinline__ uint32_t image_row(const TraceParams& P, uint32_t yl) {
+    if (P.row_block == 0) return P.row0 + yl;
+    return P.row0 + (yl / P.row_block) * P.row_stride + yl % P.row_block;
+}
+
 // SceneView over the launch's scene; with LDS, sphere/plane/light records are staged into
 // `smem` by the whole workgroup first (every thread of the block must call this).
 template <bool LDS>

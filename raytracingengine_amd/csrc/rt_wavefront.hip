@@ -73,7 +73,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_level_kernel(TraceParams P, WfA
         if (level == 0) {
             root = id;
             const uint32_t pl = root / aa, s = root % aa;
-            const uint32_t x = pl % P.width, y = P.row0 + pl / P.width;
+            const uint32_t x = pl % P.width, y = image_row(P, pl / P.width);
             o = cam;
             d = camera_dir(P, cam, x, y, static_cast<uint64_t>(y) * P.width + x,
                            static_cast<int>(s));
@@ -84,7 +84,8 @@ __global__ __launch_bounds__(kWfThreads) void wf_level_kernel(TraceParams P, WfA
             d = mk(A.ray[3 * A.cap_r + r], A.ray[4 * A.cap_r + r], A.ray[5 * A.cap_r + r]);
         }
         const uint32_t pl = root / aa, sample = root % aa;
-        const uint64_t pix = static_cast<uint64_t>(P.row0 + pl / P.width) * P.width + pl % P.width;
+        const uint64_t pix =
+            static_cast<uint64_t>(image_row(P, pl / P.width)) * P.width + pl % P.width;
         Node nd;
         nd.hit = false;
         nd.refl = false;

@@ -1,5 +1,10 @@
-"""Row-tiled multi-GPU frames: one process per GPU, each renders a contiguous
-row tile of the frame, rank 0 assembles the frame with ONE gather collective.
+"""Row-tiled multi-GPU frames: one process per GPU, each renders its rows of the
+frame, rank 0 assembles the frame with ONE gather collective.
+
+Two row plans: contiguous tiles (`block=0`), or block-cyclic rows (`block=b`: blocks of b rows
+dealt round-robin to the ranks).  Contiguous tiles of the BASELINE scenes are badly balanced
+(the slowest of 8 tiles takes 1.7x the mean on C3/C4, tools/tile_balance.py, because spheres
+cluster in the middle rows); block-cyclic rows even that out and are the default.
 
 On MI355X the process group is ``torch.distributed`` with backend ``"nccl"`` (= RCCL over
 xGMI); the gather is point-to-point into the root, so the peers' tiles arrive in parallel on
@@ -24,17 +29,38 @@ def row_tile(rank: int, world: int, height: int) -> tuple[int, int]:
     return rank * height // world, (rank + 1) * height // world
 
 
+DEFAULT_BLOCK = 16  # rows per block of the block-cyclic plan (a 16-row packet-kernel tile)
+
+
+def row_ranges(rank: int, world: int, height: int, block: int = DEFAULT_BLOCK
+               ) -> list[tuple[int, int]]:
+    """The image rows of `rank` as [r0, r1) ranges, in the order its tile stores them:
+    one contiguous tile (block == 0 or world == 1), or blocks of `block` rows starting at
+    rank*block, rank*block + world*block, ... (rt_render_opts row_block / row_cycle)."""
+    if block <= 0 or world == 1:
+        return [row_tile(rank, world, height)]
+    if not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    return [(b, min(b + block, height)) for b in range(rank * block, height, world * block)]
+
+
+def plan_rows(ranges: list[tuple[int, int]]) -> int:
+    return sum(b - a for a, b in ranges)
+
+
 def gather_rows(tile: torch.Tensor, height: int, width: int, channels: int = 3,
-                group=None) -> torch.Tensor | None:
+                group=None, block: int = 0) -> torch.Tensor | None:
     """Gather every rank's [rows, width, channels] tile to rank 0 and return the full
     [height, width, channels] frame there (None elsewhere).  Tiles are padded to the tallest
-    tile because the collective moves equal-sized buffers."""
+    tile because the collective moves equal-sized buffers; rank 0 places each rank's rows with
+    the same plan (`block`, see row_ranges)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    max_rows = -(-height // world)
-    r0, r1 = row_tile(rank, world, height)
-    if tile.shape[0] != r1 - r0:
-        raise ValueError(f"rank {rank}: tile has {tile.shape[0]} rows, expected {r1 - r0}")
+    plans = [row_ranges(r, world, height, block) for r in range(world)]
+    max_rows = max(plan_rows(p) for p in plans)
+    if tile.shape[0] != plan_rows(plans[rank]):
+        raise ValueError(f"rank {rank}: tile has {tile.shape[0]} rows, "
+                         f"expected {plan_rows(plans[rank])}")
     send = tile
     if tile.shape[0] != max_rows:
         send = torch.zeros((max_rows, width, channels), dtype=tile.dtype, device=tile.device)
@@ -45,34 +71,50 @@ def gather_rows(tile: torch.Tensor, height: int, width: int, channels: int = 3,
     dist.gather(send.contiguous(), recv, dst=0, group=group)
     if rank != 0:
         return None
-    parts = []
+    frame = torch.empty((height, width, channels), dtype=tile.dtype, device=tile.device)
     for r, buf in enumerate(recv):
-        a, b = row_tile(r, world, height)
-        parts.append(buf[: b - a])
-    return torch.cat(parts, dim=0)
+        k = 0
+        for a, b in plans[r]:
+            frame[a:b] = buf[k:k + (b - a)]
+            k += b - a
+    return frame
 
 
-def render_frame_tiled(render_rows: Callable[[int, int], torch.Tensor], height: int, width: int,
-                       channels: int = 3, group=None) -> torch.Tensor | None:
-    """Render this rank's tile with `render_rows(r0, r1)` and assemble the frame on rank 0."""
+def render_frame_tiled(render_rows: Callable[[list[tuple[int, int]]], torch.Tensor],
+                       height: int, width: int, channels: int = 3, group=None,
+                       block: int = DEFAULT_BLOCK) -> torch.Tensor | None:
+    """Render this rank's rows with `render_rows(ranges)` (a [rows, width, channels] tensor of
+    the ranges' rows, in order) and assemble the frame on rank 0."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    r0, r1 = row_tile(rank, world, height)
-    tile = render_rows(r0, r1)
-    return gather_rows(tile, height, width, channels, group)
+    tile = render_rows(row_ranges(rank, world, height, block))
+    return gather_rows(tile, height, width, channels, group, block=block)
 
 
-def hip_tile_renderer(dscene, tonemap: int | None = None, dtype=torch.float32):
-    """`render_rows` for a librtamd DeviceScene: renders [r0, r1) into a device tensor on the
-    context's stream (HDR float32, or the uint8 tonemap when `tonemap` is given)."""
+def render_opts_for(ranges: list[tuple[int, int]], rank: int, world: int, height: int,
+                    block: int, **kw):
+    """rt_render_opts selecting exactly `ranges` (row_ranges of this rank) in one launch."""
     from . import capi
 
-    width = dscene.data.camera.width
+    if block <= 0 or world == 1:
+        (r0, r1), = ranges
+        return capi.default_opts(row_begin=r0, row_end=r1, **kw)
+    return capi.default_opts(row_begin=rank * block, row_end=height, row_block=block,
+                             row_cycle=world, **kw)
 
-    def render_rows(r0: int, r1: int) -> torch.Tensor:
-        rows = r1 - r0
-        opts = capi.default_opts(tonemap=-1 if tonemap is None else tonemap, row_begin=r0,
-                                 row_end=r1)
+
+def hip_tile_renderer(dscene, rank: int, world: int, block: int = DEFAULT_BLOCK,
+                      tonemap: int | None = None, dtype=torch.float32):
+    """`render_rows` for a librtamd DeviceScene: renders this rank's rows in ONE launch into a
+    device tensor on the context's stream (HDR float32, or the uint8 tonemap when `tonemap`
+    is given)."""
+    width = dscene.data.camera.width
+    height = dscene.data.camera.height
+
+    def render_rows(ranges: list[tuple[int, int]]) -> torch.Tensor:
+        rows = plan_rows(ranges)
+        opts = render_opts_for(ranges, rank, world, height, block,
+                               tonemap=-1 if tonemap is None else tonemap)
         if tonemap is None:
             out = torch.empty((rows, width, 3), dtype=torch.float32, device="cuda")
             dscene.render_device(None, out.data_ptr(), None, opts)

@@ -168,6 +168,34 @@ def test_row_tiles_equal_full_frame(ctx, name):
     assert np.array_equal(np.concatenate([t["ldr"] for t in tiles]), full["ldr"])
 
 
+@pytest.mark.parametrize("name,world,block", [("c2", 3, 16), ("c3", 8, 16), ("glass", 4, 5),
+                                              ("mirror", 2, 7), ("mesh", 8, 1)])
+def test_block_cyclic_rows_equal_full_frame(ctx, name, world, block):
+    """Block-cyclic row sets (row_block / row_cycle, the balanced multi-GPU split): each rank's
+    single launch returns exactly its rows of the full frame, on every kernel path (packet,
+    chain, wavefront tree)."""
+    from raytracingengine_amd.distributed import plan_rows, render_opts_for, row_ranges
+    sc = make_config(name, 200, 123)
+    H = sc.camera.height
+    ds = ctx.scene(sc)
+    try:
+        full = ds.render(hdr64=True, tonemap=6)
+        frame = np.full_like(full["hdr64"], np.nan)
+        for r in range(world):
+            ranges = row_ranges(r, world, H, block)
+            out = ds.render(hdr64=True, tonemap=6,
+                            opts=render_opts_for(ranges, r, world, H, block, tonemap=6))
+            assert out["hdr64"].shape[0] == plan_rows(ranges)
+            k = 0
+            for a, b in ranges:
+                frame[a:b] = out["hdr64"][k:k + b - a]
+                assert np.array_equal(out["ldr"][k:k + b - a], full["ldr"][a:b])
+                k += b - a
+    finally:
+        ds.close()
+    assert np.array_equal(frame, full["hdr64"])
+
+
 def test_deterministic(ctx):
     sc = make_config("c3", 640, 360)
     a = _render(ctx, sc, hdr64=True)
