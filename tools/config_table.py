@@ -10,14 +10,22 @@ from oracle import pyoracle as po
 from raytracingengine_amd import capi
 from raytracingengine_amd.configs import make_config
 
-CPU_SCALE = {"c1": 4, "c2": 4, "c3": 8, "c4": 16, "c5": 8, "mirror": 4, "glass": 4, "mesh": 4}
+CPU_SCALE = {"c1": 4, "c2": 4, "c3": 8, "c4": 16, "c5": 8, "mirror": 4, "glass": 4, "mesh": 4,
+             "c1_aa32": 10}
+
+
+def config(name, w=None, h=None):
+    """`c1_aa32`: the reference main()'s own sampling (Camera::antiAliasingAmount = 32)."""
+    if name == "c1_aa32":
+        return make_config("c1", w, h, aa=32) if w else make_config("c1", aa=32)
+    return make_config(name, w, h) if w else make_config(name)
 threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
 ctx = capi.Context(0)
 s = torch.cuda.Stream(); ctx.set_stream(s.cuda_stream)
 rows = []
-names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5", "mirror", "glass", "mesh"]
+names = sys.argv[1:] or ["c1", "c1_aa32", "c2", "c3", "c4", "c5", "mirror", "glass", "mesh"]
 for name in names:
-    sc = make_config(name)
+    sc = config(name)
     ds = ctx.scene(sc)
     W, H = sc.camera.width, sc.camera.height
     hdr = torch.empty(W * H * 3, dtype=torch.float64, device="cuda")
@@ -32,12 +40,12 @@ for name in names:
             ds.render_device(hdr.data_ptr(), None, ldr.data_ptr(), o)
         st = ctx.stats(); best = min(best, st.kernel_ms / st.launches)
     ds.close()
-    row = {"config": name, "resolution": [W, H], "spheres": len(sc.spheres),
+    row = {"config": name, "resolution": [W, H], "aa": sc.camera.antiAliasingAmount, "spheres": len(sc.spheres),
            "planes": len(sc.planes), "lights": len(sc.lights), "rays_per_frame": rays,
            "gpu_ms_per_frame": round(best, 4), "gpu_mrays_s": round(rays / best / 1e3, 1)}
     if po.ref_available():
         k = CPU_SCALE[name]
-        small = make_config(name, W // k, H // k)
+        small = config(name, W // k, H // k)
         dss = ctx.scene(small)
         b = dss.render(hdr64=False, stats=True)
         dss.close()
