@@ -292,6 +292,15 @@ def test_invalid_arguments_raise(ctx):
         with pytest.raises(capi.RtError) as e:
             ds.render(hdr64=True, tonemap=9)
         assert e.value.status == capi.RT_ERR_INVALID_ARG
+        with pytest.raises(capi.RtError) as e:  # block-cyclic rows need a block height
+            ds.render(hdr64=True, row_cycle=2, row_block=0)
+        assert e.value.status == capi.RT_ERR_INVALID_ARG
+        # a cycle of 1 is the contiguous range; blocks past row_end are clipped
+        one = ds.render(hdr64=True, row_cycle=1, row_block=4)
+        full = ds.render(hdr64=True)
+        assert np.array_equal(one["hdr64"], full["hdr64"])
+        tail = ds.render(hdr64=True, row_begin=12, row_cycle=3, row_block=5)
+        assert np.array_equal(tail["hdr64"], full["hdr64"][12:16])
     finally:
         ds.close()
     mirror = make_config("mirror", 16, 16)
