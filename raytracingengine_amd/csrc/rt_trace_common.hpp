@@ -240,6 +240,68 @@ __device__ __forceinline__ double transmittance(const SceneView& S, d3 o, d3 d, 
     return sclamp(T, 0.0, 1.0);
 }
 
+// computeTransmittance for scenes without transparency (the direct and chain paths: any
+// transparent material selects the tree path), where it can only return 1 or 0 and is decided
+// by its first closest hit t* (blocked iff bias < t* < maxDist).  Each sphere is classified with
+// the reference's FP64 discriminant, a FP32 square root and one shared reciprocal of 2a under an
+// explicit error bound Δ of the roots; planes by comparing num with x·denom (1e-9 relative
+// margin) instead of dividing.  Any root within Δ of a threshold (1e-6, bias, maxDist), any near
+// hit, triangles, or values outside the fast ranges return -1 and the exact march runs.
+// Same classification as the packet kernel's pk_occlusion (rt_packet.hip), over every sphere.
+__device__ __forceinline__ int occlusion_opaque(const SceneView& S, d3 o, d3 d, double max_dist,
+                                                double bias) {
+    if (S.nt > 0) return -1;
+    const double a = dot(d, d);
+    const double two_a = 2.0 * a, four_a = 4.0 * a;
+    if (!(two_a > 0.0)) return -1;
+    const double inv2a = 1.0 / two_a;
+    bool blocked = false, undecided = false;
+    for (int i = 0; i < S.ns; ++i) {
+        const double* s = S.sph + kSphStride * i;
+        const d3 oc = o - mk(s[0], s[1], s[2]);
+        const double b = 2.0 * dot(oc, d);
+        const double cc = dot(oc, oc) - s[3];
+        const double disc = b * b - four_a * cc;
+        if (disc < 0.0) continue;  // miss, exactly as the reference decides it
+        if (!(disc == 0.0 || (disc > 1e-30 && disc < 1e30))) {
+            undecided = true;
+            continue;
+        }
+        // |sq − fl(√disc)| ≤ 5e-7·√disc, so both roots are within Δ of the reference's
+        const double sq = static_cast<double>(sqrtf(static_cast<float>(disc)));
+        const double delta = 2e-6 * (fabs(b) + sq) * inv2a;
+        double t = (-b - sq) * inv2a;
+        if (!(t >= 1e-6 + delta)) {
+            if (!(t < 1e-6 - delta)) {
+                undecided = true;
+                continue;
+            }
+            t = (-b + sq) * inv2a;
+            if (t < 1e-6 - delta) continue;
+            if (!(t >= 1e-6 + delta)) {
+                undecided = true;
+                continue;
+            }
+        }
+        if (t >= max_dist + delta) continue;
+        if (t > bias + delta && t < max_dist - delta) blocked = true;
+        else undecided = true;
+    }
+    for (int i = 0; i < S.np; ++i) {
+        const double* p = S.pl + kPlStride * i;
+        const d3 n = mk(p[3], p[4], p[5]);
+        const double denom = dot(n, d);
+        if (!(fabs(denom) > 1e-6)) continue;
+        const double num = dot(mk(p[0], p[1], p[2]) - o, n);
+        const double A = denom > 0.0 ? num : -num, B = fabs(denom);
+        if (A < -1e-300 * B) continue;
+        if (A >= max_dist * B * (1.0 + 1e-9)) continue;
+        if (A > bias * B * (1.0 + 1e-9) && A < max_dist * B * (1.0 - 1e-9)) blocked = true;
+        else undecided = true;
+    }
+    return undecided ? -1 : (blocked ? 0 : 1);
+}
+
 struct Mat {
     d3 color;
     double shininess, specular, transparency, ior;
@@ -250,7 +312,7 @@ __device__ __forceinline__ Mat load_mat(const double* m) {
 }
 
 // One iteration of directLightning's light loop (Scene.h:86-124).  E = color*intensity.
-template <bool COUNT>
+template <bool COUNT, bool OPQ>
 __device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 view, const Mat& m,
                                            d3 lpos, d3 E, double bias, d3& diff, d3& spec,
                                            Counts& cnt) {
@@ -262,7 +324,13 @@ __device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 vi
     if (ndl <= 0.0) return;
     if (dist <= bias) return;
     if (COUNT) cnt.shadow++;
-    const double T = transmittance(S, P + n * bias, L, dist - bias, bias);
+    double T;
+    if constexpr (OPQ) {
+        const int occ = occlusion_opaque(S, P + n * bias, L, dist - bias, bias);
+        T = occ >= 0 ? static_cast<double>(occ) : transmittance(S, P + n * bias, L, dist - bias, bias);
+    } else {
+        T = transmittance(S, P + n * bias, L, dist - bias, bias);
+    }
     if (T <= bias) return;
     const double inv_d2 = 1.0 / (dist * dist);
     diff = diff + ((E * inv_d2) * ndl) * T;
@@ -277,7 +345,7 @@ __device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 vi
 }
 
 // Scene::directLightning (Scene.h:79-129), plus the build-defined area-light samples.
-template <bool COUNT>
+template <bool COUNT, bool OPQ>
 __device__ __forceinline__ d3 direct(const SceneView& S, const TraceParams& P, d3 hp, d3 view,
                                      d3 n_in, const Mat& m, uint64_t pix, uint32_t sample,
                                      int depth, Counts& cnt) {
@@ -286,7 +354,7 @@ __device__ __forceinline__ d3 direct(const SceneView& S, const TraceParams& P, d
     d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
     for (int i = 0; i < S.nl; ++i) {
         const double* l = S.lt + kLtStride * i;
-        light_term<COUNT>(S, hp, n, view, m, mk(l[0], l[1], l[2]), mk(l[3], l[4], l[5]), bias,
+        light_term<COUNT, OPQ>(S, hp, n, view, m, mk(l[0], l[1], l[2]), mk(l[3], l[4], l[5]), bias,
                           diff, spec, cnt);
     }
     if (P.al_samples > 0) {
@@ -302,7 +370,7 @@ __device__ __forceinline__ d3 direct(const SceneView& S, const TraceParams& P, d
             const double fu = (static_cast<double>(s % P.al_k) + r1) / k;
             const double fv = (static_cast<double>(s / P.al_k) + r2) / k;
             const d3 lp = (corner + eu * fu) + ev * fv;
-            light_term<COUNT>(S, hp, n, view, m, lp, E, bias, diff, spec, cnt);
+            light_term<COUNT, OPQ>(S, hp, n, view, m, lp, E, bias, diff, spec, cnt);
         }
     }
     return hmul(m.color, diff) + spec * m.specular;
@@ -341,7 +409,7 @@ __device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, 
     const d3 n = front ? gn : -gn;
     const d3 view = -inc;
     const double tr = sclamp(m.transparency, 0.0, 1.0);
-    const d3 local = direct<COUNT>(S, P, hp, view, n, m, pix, sample, depth, cnt);
+    const d3 local = direct<COUNT, !TREE>(S, P, hp, view, n, m, pix, sample, depth, cnt);
     d3 fin = mk(0.0, 0.0, 0.0);
     if (tr < 1.0) fin = fin + local * (1.0 - tr);
     nd.value = fin;
