@@ -64,6 +64,12 @@ struct TraceParams {
     const uint8_t* redo;  // generic kernels: when set, only pixels with a flagged sample run
 };
 
+// Doubles of the scene image the generic kernels stage into LDS (spheres, planes, lights).
+__host__ __device__ inline size_t scene_doubles(const TraceParams& p) {
+    return static_cast<size_t>(kSphStride) * p.ns + static_cast<size_t>(kPlStride) * p.np +
+           static_cast<size_t>(kLtStride) * p.nl;
+}
+
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
                         hipStream_t stream);
 hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specular,

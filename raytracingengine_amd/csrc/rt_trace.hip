@@ -19,11 +19,13 @@
 
 namespace rtamd {
 
-template <int PATH, bool COUNT, bool LDS>
+template <int PATH, bool COUNT, bool LDS, bool LSTK = false>
 __global__ __launch_bounds__(kTileW * kTileH) void trace_kernel(TraceParams P) {
     extern __shared__ double smem[];
-    const SceneView S = stage_scene<LDS>(P, smem, threadIdx.y * kTileW + threadIdx.x,
-                                         kTileW * kTileH);
+    const int tid = threadIdx.y * kTileW + threadIdx.x;
+    const SceneView S = stage_scene<LDS>(P, smem, tid, kTileW * kTileH);
+    // chain stack in LDS after the staged scene (scene_doubles() of them when LDS)
+    double* lstk = smem + (LDS ? scene_doubles(P) : 0) + tid;
     const uint32_t x = blockIdx.x * kTileW + threadIdx.x;
     const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
     Counts cnt{0u, 0u};
@@ -48,7 +50,8 @@ __global__ __launch_bounds__(kTileW * kTileH) void trace_kernel(TraceParams P) {
             if constexpr (PATH == kPathDirect)
                 c = trace_direct<COUNT>(S, P, cam, dir, pix, static_cast<uint32_t>(s), cnt);
             else if constexpr (PATH == kPathChain)
-                c = trace_chain<COUNT>(S, P, cam, dir, pix, static_cast<uint32_t>(s), cnt);
+                c = trace_chain<COUNT, LSTK>(S, P, cam, dir, pix, static_cast<uint32_t>(s), cnt,
+                                             lstk, kTileW * kTileH);
             else
                 c = trace_tree<COUNT>(S, P, cam, dir, pix, static_cast<uint32_t>(s), cnt);
             acc = acc + c;
@@ -71,23 +74,43 @@ __global__ __launch_bounds__(kTileW * kTileH) void trace_kernel(TraceParams P) {
     }
 }
 
-template <int PATH, bool COUNT, bool LDS>
+// LDS chain stack: 4 doubles (value xyz, weight) per pending level per thread; a chain keeps
+// at most max_recursion - 1 levels pending (the last one folds with the sky at once)
+static size_t chain_stack_bytes(const TraceParams& p) {
+    return sizeof(double) * 4 * static_cast<size_t>(p.max_rec > 1 ? p.max_rec - 1 : 0) *
+           kTileW * kTileH;
+}
+
+template <int PATH, bool COUNT, bool LDS, bool LSTK>
 static hipError_t launch_one(const TraceParams& p, size_t lds_bytes, hipStream_t stream) {
     const dim3 block(kTileW, kTileH);
     const dim3 grid((p.width + kTileW - 1) / kTileW, (p.rows + kTileH - 1) / kTileH);
-    hipLaunchKernelGGL((trace_kernel<PATH, COUNT, LDS>), grid, block, LDS ? lds_bytes : 0,
-                       stream, p);
+    const size_t smem = (LDS ? lds_bytes : 0) + (LSTK ? chain_stack_bytes(p) : 0);
+    hipLaunchKernelGGL((trace_kernel<PATH, COUNT, LDS, LSTK>), grid, block, smem, stream, p);
     return hipGetLastError();
+}
+
+template <int PATH, bool LSTK>
+static hipError_t launch_lds(const TraceParams& p, bool count, bool lds, size_t lds_bytes,
+                             hipStream_t stream) {
+    if (count)
+        return lds ? launch_one<PATH, true, true, LSTK>(p, lds_bytes, stream)
+                   : launch_one<PATH, true, false, LSTK>(p, lds_bytes, stream);
+    return lds ? launch_one<PATH, false, true, LSTK>(p, lds_bytes, stream)
+               : launch_one<PATH, false, false, LSTK>(p, lds_bytes, stream);
 }
 
 template <int PATH>
 static hipError_t launch_path(const TraceParams& p, bool count, bool lds, size_t lds_bytes,
                               hipStream_t stream) {
-    if (count)
-        return lds ? launch_one<PATH, true, true>(p, lds_bytes, stream)
-                   : launch_one<PATH, true, false>(p, lds_bytes, stream);
-    return lds ? launch_one<PATH, false, true>(p, lds_bytes, stream)
-               : launch_one<PATH, false, false>(p, lds_bytes, stream);
+    if constexpr (PATH == kPathChain) {
+        // reflection chains keep their pending levels in LDS when two 256-thread workgroups
+        // still fit a CU (the kernel runs at 2 waves/SIMD anyway): max_recursion 10 = 72 KiB
+        const size_t total = (lds ? lds_bytes : 0) + chain_stack_bytes(p);
+        if (p.max_rec > 1 && total <= 80 * 1024)
+            return launch_lds<PATH, true>(p, count, lds, lds_bytes, stream);
+    }
+    return launch_lds<PATH, false>(p, count, lds, lds_bytes, stream);
 }
 
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
@@ -129,7 +152,7 @@ __global__ __launch_bounds__(256) void trace_rays_kernel(TraceParams P, const do
         const d3 d = mk(r[3], r[4], r[5]);
         d3 c;
         if constexpr (PATH == kPathDirect) c = trace_direct<COUNT>(S, P, o, d, i, 0u, cnt);
-        else if constexpr (PATH == kPathChain) c = trace_chain<COUNT>(S, P, o, d, i, 0u, cnt);
+        else if constexpr (PATH == kPathChain) c = trace_chain<COUNT, false>(S, P, o, d, i, 0u, cnt);
         else c = trace_tree<COUNT>(S, P, o, d, i, 0u, cnt);
         out[3 * i + 0] = c.x;
         out[3 * i + 1] = c.y;

@@ -454,11 +454,15 @@ __device__ __forceinline__ d3 trace_direct(const SceneView& S, const TraceParams
 
 // TraceRay for opaque scenes: a linear reflection chain.  Levels are pushed front-to-back and
 // folded back-to-front, final_k = value_k + child_k * rw_k, the reference's rounding order.
-template <bool COUNT>
+// The chain's pending levels (value, weight) live either in private memory (scratch) or, when
+// the workgroup has room, in LDS: `lstk` points at this thread's column of a structure-of-arrays
+// block [level][component][thread] with `stride` = threads per workgroup (conflict-free).
+template <bool COUNT, bool LSTK>
 __device__ __forceinline__ d3 trace_chain(const SceneView& S, const TraceParams& P, d3 o, d3 d,
-                                          uint64_t pix, uint32_t sample, Counts& cnt) {
-    d3 base[kMaxDepth];
-    double w[kMaxDepth];
+                                          uint64_t pix, uint32_t sample, Counts& cnt,
+                                          double* lstk = nullptr, int stride = 0) {
+    d3 base[LSTK ? 1 : kMaxDepth];
+    double w[LSTK ? 1 : kMaxDepth];
     int depth = 0;
     d3 leaf;
     while (true) {
@@ -471,14 +475,35 @@ __device__ __forceinline__ d3 trace_chain(const SceneView& S, const TraceParams&
             leaf = nd.value;
             break;
         }
-        base[depth] = nd.value;
-        w[depth] = nd.rw;
+        if (depth + 1 >= P.max_rec) {
+            // the child is TraceRay at depth maxRecursion: the sky (Scene.h:132-134); fold
+            // this level right away (the same two operations the stack would do)
+            leaf = nd.value + sky(nd.rd) * nd.rw;
+            break;
+        }
+        if constexpr (LSTK) {
+            double* f = lstk + 4 * depth * stride;
+            f[0] = nd.value.x;
+            f[stride] = nd.value.y;
+            f[2 * stride] = nd.value.z;
+            f[3 * stride] = nd.rw;
+        } else {
+            base[depth] = nd.value;
+            w[depth] = nd.rw;
+        }
         o = nd.ro;
         d = nd.rd;
         ++depth;
     }
     d3 acc = leaf;
-    for (int k = depth - 1; k >= 0; --k) acc = base[k] + acc * w[k];
+    for (int k = depth - 1; k >= 0; --k) {
+        if constexpr (LSTK) {
+            const double* f = lstk + 4 * k * stride;
+            acc = mk(f[0], f[stride], f[2 * stride]) + acc * f[3 * stride];
+        } else {
+            acc = base[k] + acc * w[k];
+        }
+    }
     return acc;
 }
 
