@@ -60,26 +60,6 @@ constexpr int kFeatAll = 15;
 #define RT_PACKET_LEAN_WAVES 4
 #endif
 
-// ------------------------------------------------------------------ diagnostic phase stamps
-// -DRT_STAMPS builds (tools/stamp_phases.py) accumulate s_memtime cycles per kernel phase and
-// wave into a device array read back by rt_debug_stamps(); product builds compile them away.
-#ifdef RT_STAMPS
-__device__ unsigned long long g_stamps[16];
-struct Stamps {
-    uint64_t prev;
-    uint64_t acc[12];
-};
-#define RT_STAMP(ST, i)                                             \
-    do {                                                            \
-        const uint64_t now_ = __builtin_amdgcn_s_memtime();         \
-        (ST).acc[i] += now_ - (ST).prev;                            \
-        (ST).prev = now_;                                           \
-    } while (0)
-#else
-struct Stamps {};
-#define RT_STAMP(ST, i) ((void)0)
-#endif
-
 // ------------------------------------------------------------------ wave reductions (FP32)
 // Every lane must be active.  Four DPP steps reduce each 16-lane row (quad xor-1, quad xor-2,
 // half-mirror, mirror: every lane of a row ends with the row's result), then the four row
@@ -535,7 +515,7 @@ template <int MAXC, int FEAT, bool COUNT>
 __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P, d3 n, d3 view,
                                          const Hit& h, d3 lpos, d3 E, d3 lcenter, double lrad,
                                          double bias, int nchunks, d3& diff, d3& spec,
-                                         Counts& cnt, Stamps& ST) {
+                                         Counts& cnt) {
     const d3 v = lpos - P;
     const double dist = length(v);
     const bool reach = active && !(dist <= 0.0);
@@ -561,11 +541,9 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
                               : cull_capsule<MAXC>(S, c, R, lcenter, lrad);
     if (!need) return;
     if (COUNT) cnt.shadow++;
-    RT_STAMP(ST, 5);
     const int occ = pk_occlusion<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
     double T = occ == 1 ? 0.0 : 1.0;
     if (occ == 2) T = pk_transmittance<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
-    RT_STAMP(ST, 6);
     if (T <= bias) return;
     const double inv_d2 = 1.0 / (dist * dist);
     diff = diff + ((E * inv_d2) * ndl) * T;
@@ -628,11 +606,6 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
     S.nt = P.nt;
     S.nl = nl;
     const int nchunks = (ns + 63) / 64;
-    Stamps ST;
-#ifdef RT_STAMPS
-    ST.prev = __builtin_amdgcn_s_memtime();
-    for (int i = 0; i < 12; ++i) ST.acc[i] = 0;
-#endif
 
     const int lane = tid & 63, wave = tid >> 6;
     const uint32_t x = blockIdx.x * (kPkW * kWgWavesX) + (wave % kWgWavesX) * kPkW + (lane % kPkW);
@@ -668,7 +641,6 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
         sx += jx;
         sy += jy;
         const d3 d = unit(mk(sx, sy, cam.z + P.focal) - cam);
-        RT_STAMP(ST, 1);
 
         d3 col;
         if (P.max_rec <= 0) {
@@ -683,13 +655,11 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
             const bool ok = isfinite(cos_min) && cos_min > 0.0;  // cones narrower than 90°
             const Masks<MAXC> M = ok ? cull_cone<MAXC>(S, cam, axis, cos_min)
                                      : all_candidates<MAXC>(ns);
-            RT_STAMP(ST, 2);
             Hit h;
             h.t = 0.0;
             h.kind = 0;
             h.idx = 0;
             const bool hit = valid && closest_camera<MAXC, FEAT>(S, M, nchunks, cam, d, h);
-            RT_STAMP(ST, 3);
             // shading inputs (Scene.h:147-154); misses carry harmless placeholders
             const d3 hp = cam + d * h.t;
             const d3 gn = hit ? pk_normal(S, h, hp) : mk(0.0, 1.0, 0.0);
@@ -698,14 +668,12 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
             const d3 n0 = front ? gn : -gn;
             const d3 view = -inc;
             const d3 n = unit(n0);  // directLightning's own normalize (Scene.h:81)
-            RT_STAMP(ST, 4);
             d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
             for (int l = 0; l < nl; ++l) {
                 const double* lp = S.lt + kLtStride * l;
                 const d3 L = mk(lp[0], lp[1], lp[2]);
                 pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, L, mk(lp[3], lp[4], lp[5]),
-                                            L, 0.0, bias, nchunks, diff, spec, cnt, ST);
-                RT_STAMP(ST, 7);
+                                            L, 0.0, bias, nchunks, diff, spec, cnt);
             }
             if constexpr ((FEAT & kFeatArea) != 0) {
                 if (P.al_samples > 0) {
@@ -723,7 +691,7 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
                         const double fv = (static_cast<double>(q / P.al_k) + r2) / k;
                         const d3 lpos = (corner + eu * fu) + ev * fv;
                         pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, lpos, E, al_c, al_r,
-                                                    bias, nchunks, diff, spec, cnt, ST);
+                                                    bias, nchunks, diff, spec, cnt);
                     }
                 }
             }
@@ -740,7 +708,6 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
         }
         acc = acc + col;
         samples += 1;
-        RT_STAMP(ST, 8);
     }
     if (valid) {
         // accumulated / samples (Scene.h:298-300); x / 1.0 == x, so AA=1 skips the division
@@ -766,13 +733,6 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
             P.ldr[3 * o + 2] = b;
         }
     }
-    RT_STAMP(ST, 9);
-#ifdef RT_STAMPS
-    if (lane == 0) {
-        for (int i = 0; i < 12; ++i) atomicAdd(&g_stamps[i], ST.acc[i]);
-        atomicAdd(&g_stamps[15], 1ull);
-    }
-#endif
     if constexpr (COUNT) {
         uint32_t t = cnt.trace, sh = cnt.shadow;
         for (int off = 32; off > 0; off >>= 1) {
@@ -828,17 +788,3 @@ hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specu
 }
 
 }  // namespace rtamd
-
-#ifdef RT_STAMPS
-extern "C" int rt_debug_stamps(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_stamps), sizeof(rtamd::g_stamps)) !=
-        hipSuccess)
-        return 1;
-    if (reset) {
-        static const unsigned long long zero[16] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(rtamd::g_stamps), zero, sizeof zero) != hipSuccess)
-            return 1;
-    }
-    return 0;
-}
-#endif
