@@ -160,6 +160,7 @@ typedef struct rt_render_opts {
 #define RT_FLAG_COUNT_RAYS 0x1   /* also run the ray-counting pass (fills rt_stats counts)   */
 #define RT_FLAG_TIME_KERNEL 0x2  /* bracket each render launch with HIP events              */
 #define RT_FLAG_GENERIC_KERNEL 0x4 /* ablation: bypass the packet-culled kernel              */
+#define RT_FLAG_NO_BVH 0x8         /* ablation: test every triangle (no triangle BVH)          */
 
 /* Fills opts with the reference defaults: max_recursion 10, bias 1e-3, tonemap ACES,
  * full image, seed 0x5EED, no flags. */

@@ -27,6 +27,7 @@ TONEMAP_ALL = 7
 RT_FLAG_COUNT_RAYS = 0x1
 RT_FLAG_TIME_KERNEL = 0x2
 RT_FLAG_GENERIC_KERNEL = 0x4
+RT_FLAG_NO_BVH = 0x8
 
 # Every symbol include/rt_capi.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED = [

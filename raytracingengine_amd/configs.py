@@ -41,7 +41,8 @@ class SplitMix64:
         return lo + (hi - lo) * ((self.next_u64() >> 11) * 2.0 ** -53)
 
 
-CONFIG_IDS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5, "mirror": 6, "glass": 7, "mesh": 8}
+CONFIG_IDS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5, "mirror": 6, "glass": 7, "mesh": 8,
+              "bigmesh": 9}
 
 # name -> (width, height, n_spheres, plane list, n_lights)
 _PLANE_SPECS = {
@@ -169,6 +170,57 @@ def mesh_scene(width=1920, height=1080, aa=1) -> SceneData:
     return sc
 
 
+def _icosphere(radius: float, levels: int):
+    """Icosahedron subdivided `levels` times (20·4^levels triangles), vertices on the sphere."""
+    tris = _icosahedron(1.0)
+
+    def norm(p):
+        n = math.sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2])
+        return (p[0] / n, p[1] / n, p[2] / n)
+
+    tris = [tuple(norm(v) for v in t) for t in tris]
+    for _ in range(levels):
+        out = []
+        for a, b, c in tris:
+            ab = norm(tuple((x + y) / 2 for x, y in zip(a, b)))
+            bc = norm(tuple((x + y) / 2 for x, y in zip(b, c)))
+            ca = norm(tuple((x + y) / 2 for x, y in zip(c, a)))
+            out += [(a, ab, ca), (ab, b, bc), (ca, bc, c), (ab, bc, ca)]
+        tris = out
+    return [tuple(tuple(radius * x for x in v) for v in t) for t in tris]
+
+
+def _terrain(n: int, size: float, rng: SplitMix64):
+    """n×n quads (2n² triangles) of a bumpy height field over [-size, size]²."""
+    h = [[rng.uniform(-0.8, 0.8) for _ in range(n + 1)] for _ in range(n + 1)]
+    def p(i, j):
+        return (-size + 2 * size * i / n, h[i][j], -size + 2 * size * j / n)
+    tris = []
+    for i in range(n):
+        for j in range(n):
+            tris.append((p(i, j), p(i + 1, j), p(i + 1, j + 1)))
+            tris.append((p(i, j), p(i + 1, j + 1), p(i, j + 1)))
+    return tris
+
+
+def bigmesh_scene(width=1920, height=1080, aa=1) -> SceneData:
+    """Models at scale ('Models at scale need a BVH'): a 5120-triangle icosphere
+    and a 3200-triangle terrain, plus spheres, a back plane and two lights; opaque, no
+    specular, so it renders through the packet kernel with the triangle BVH."""
+    rng = SplitMix64(0x5EED0000 + CONFIG_IDS["bigmesh"])
+    cam = Camera((0.0, 0.0, -25.0), width / 2.0, width, height, 0.0, 200.0, aa)
+    sc = SceneData(cam, name="bigmesh")
+    sc.add_sphere((7.0, -3.0, 4.0), 2.0, Material((0.9, 0.4, 0.2)))
+    sc.add_sphere((-9.0, 4.0, 8.0), 1.5, Material((0.3, 0.5, 0.9)))
+    p, n, col = _PLANE_SPECS["back"]
+    sc.add_plane(p, n, Material(col))
+    sc.add_model(_icosphere(4.0, 4), (-3.0, 1.0, 6.0), Material((0.8, 0.8, 0.85)))
+    sc.add_model(_terrain(40, 14.0, rng), (0.0, -9.0, 6.0), Material((0.4, 0.7, 0.3)))
+    sc.add_light((0.0, 12.0, -10.0), (1.0, 1.0, 1.0), 250.0)
+    sc.add_light((9.0, 7.0, -8.0), (1.0, 0.8, 0.6), 90.0)
+    return sc
+
+
 def make_config(name: str, width: int | None = None, height: int | None = None,
                 aa: int = 1) -> SceneData:
     """Build a named scene at its BASELINE resolution (or at width×height)."""
@@ -186,6 +238,8 @@ def make_config(name: str, width: int | None = None, height: int | None = None,
         sc = glass_scene(aa=aa)
     elif name == "mesh":
         sc = mesh_scene(aa=aa)
+    elif name == "bigmesh":
+        sc = bigmesh_scene(aa=aa)
     else:
         raise KeyError(f"unknown config {name!r}; known: {sorted(CONFIG_IDS)}")
     if width is not None:

@@ -101,6 +101,8 @@ struct rt_scene {
     double max_specular = 0.0;  // NaN-aware: stored as +inf when a NaN specular exists
     bool has_area = false;
     rt_area_light area{};
+    size_t off_bvh = 0, off_bvh_tri = 0;  // triangle BVH, when bvh_nodes > 0
+    int32_t bvh_nodes = 0;
 };
 
 namespace {
@@ -202,6 +204,10 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
     p.pl_mat = base + sc->off_pl_mat;
     p.tri = base + sc->off_tri;
     p.tri_mat = base + sc->off_tri_mat;
+    if (sc->bvh_nodes > 0 && !(opts.flags & RT_FLAG_NO_BVH)) {
+        p.bvh = base + sc->off_bvh;
+        p.bvh_tri = reinterpret_cast<const int32_t*>(base + sc->off_bvh_tri);
+    }
     p.lt = base + sc->off_lt;
     p.ns = sc->ns;
     p.np = sc->np;
@@ -513,6 +519,20 @@ rt_status rt_scene_create(rt_context* ctx, const rt_scene_desc* d, rt_scene** ou
     }
     sc->any_transparent = transparent;
     sc->max_specular = max_spec;
+
+    // triangle BVH (rt_bvh.cpp) appended to the same allocation: nodes, then the leaf-order
+    // triangle ids packed two per double slot
+    if (sc->nt >= kBvhMinTris) {
+        std::vector<double> nodes;
+        std::vector<int32_t> order;
+        build_triangle_bvh(&h[sc->off_tri], sc->nt, nodes, order);
+        sc->off_bvh = h.size();
+        sc->off_bvh_tri = sc->off_bvh + nodes.size();
+        h.resize(sc->off_bvh_tri + (order.size() + 1) / 2 + 2, 0.0);
+        std::memcpy(&h[sc->off_bvh], nodes.data(), nodes.size() * sizeof(double));
+        std::memcpy(&h[sc->off_bvh_tri], order.data(), order.size() * sizeof(int32_t));
+        sc->bvh_nodes = static_cast<int32_t>(nodes.size() / kBvhNodeStride);
+    }
 
     hipError_t e = sc->buf.ensure(h.size() * sizeof(double));
     if (e == hipSuccess)

@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace rtamd {
 
 // Device scene records (doubles per record).  Layout in HBM is one allocation, record arrays
@@ -16,6 +18,9 @@ constexpr int kTriStride = 12;  // a0(3) e1(3) e2(3) n(3) (translated v0 and edg
 constexpr int kLtStride = 8;    // px py pz Ex Ey Ez - -  (E = color*intensity, Scene.h:110)
 constexpr int kMatStride = 8;   // r g b shininess specular transparency ior -
 
+constexpr int kBvhNodeStride = 8;  // triangle BVH node: lo xyz, hi xyz, {first, count}
+constexpr int kBvhMinTris = 32;    // scenes with fewer triangles test them all (no BVH)
+constexpr int kBvhStack = 64;      // traversal stack entries (build depth <= 48)
 constexpr int kMaxDepth = 16;   // deepest recursion the CHAIN/TREE kernels keep a stack for
 constexpr int kTileW = 64;      // pixels per wave along a row (one wave = 64 contiguous pixels)
 constexpr int kTileH = 4;       // rows per workgroup (256 threads)
@@ -62,7 +67,13 @@ struct TraceParams {
     int32_t _pad;
     unsigned long long* counters;  // [trace, shadow] — only written by the counting variant
     const uint8_t* redo;  // generic kernels: when set, only pixels with a flagged sample run
+    const double* bvh;       // triangle BVH nodes (rt_bvh.cpp), or null: test every triangle
+    const int32_t* bvh_tri;  // triangle ids in leaf order
 };
+
+// Host: builds the triangle BVH over the uploaded triangle records (kTriStride doubles each).
+void build_triangle_bvh(const double* tri, int nt, std::vector<double>& nodes,
+                        std::vector<int32_t>& order);
 
 // Doubles of the scene image the generic kernels stage into LDS (spheres, planes, lights).
 __host__ __device__ inline size_t scene_doubles(const TraceParams& p) {

@@ -99,6 +99,8 @@ struct PacketScene {
     const double* lt;    // LDS: point lights
     const double* tri;   // HBM
     const double* mat;   // HBM: material table [spheres | planes | triangles]
+    const double* bvh;   // HBM: triangle BVH, or null
+    const int32_t* bvh_tri;
     int ns, np, nt, nl;
 };
 
@@ -288,23 +290,13 @@ template <int FEAT>
 __device__ __forceinline__ void triangles(const PacketScene& S, d3 o, d3 d, bool& found,
                                           double& best, int& kind, int& idx) {
     if (!(FEAT & kFeatTris)) return;
+    if (S.bvh) {
+        bvh_triangles(S.tri, S.bvh, S.bvh_tri, o, d, found, best, kind, idx);
+        return;
+    }
     for (int i = 0; i < S.nt; ++i) {
-        const double* q = S.tri + kTriStride * i;
-        const d3 a0 = mk(q[0], q[1], q[2]);
-        const d3 e1 = mk(q[3], q[4], q[5]);
-        const d3 e2 = mk(q[6], q[7], q[8]);
-        const d3 hv = cross(d, e2);
-        const double det = dot(e1, hv);
-        if (det > -1e-6 && det < 1e-6) continue;
-        const double f = 1.0 / det;
-        const d3 sv = o - a0;
-        const double u = f * dot(sv, hv);
-        if (u < 0.0 || u > 1.0) continue;
-        const d3 qv = cross(sv, e1);
-        const double v = f * dot(d, qv);
-        if (v < 0.0 || u + v > 1.0) continue;
-        const double t = f * dot(e2, qv);
-        if (t > 1e-6 && (!found || t < best)) {
+        double t;
+        if (tri_hit(S.tri, i, o, d, t) && (!found || t < best)) {
             found = true;
             best = t;
             kind = 3;
@@ -601,6 +593,8 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
     S.lt = s_lt;
     S.tri = P.tri;
     S.mat = P.sph_mat;
+    S.bvh = P.bvh;
+    S.bvh_tri = P.bvh_tri;
     S.ns = ns;
     S.np = np;
     S.nt = P.nt;

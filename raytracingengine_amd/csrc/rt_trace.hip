@@ -136,6 +136,8 @@ __device__ __forceinline__ SceneView global_view(const TraceParams& P) {
     S.sph_mat = P.sph_mat;
     S.pl_mat = P.pl_mat;
     S.tri_mat = P.tri_mat;
+    S.bvh = P.bvh;
+    S.bvh_tri = P.bvh_tri;
     return S;
 }
 

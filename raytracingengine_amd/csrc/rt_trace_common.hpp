@@ -22,6 +22,8 @@ struct SceneView {
     const double* sph_mat;
     const double* pl_mat;
     const double* tri_mat;
+    const double* bvh;       // triangle BVH (null: every triangle is tested)
+    const int32_t* bvh_tri;
     int ns, np, nt, nl;
 };
 
@@ -35,6 +37,107 @@ struct Counts {
     uint32_t trace;
     uint32_t shadow;
 };
+
+// Triangle::Intersect (Shape.h:202-220), Möller–Trumbore with the reference's operation order;
+// true with t when the triangle is hit at t > 1e-6.
+__device__ __forceinline__ bool tri_hit(const double* tri, int i, d3 o, d3 d, double& t) {
+    const double* q = tri + kTriStride * i;
+    const d3 a0 = mk(q[0], q[1], q[2]);
+    const d3 e1 = mk(q[3], q[4], q[5]);
+    const d3 e2 = mk(q[6], q[7], q[8]);
+    const d3 hv = cross(d, e2);
+    const double det = dot(e1, hv);
+    if (det > -1e-6 && det < 1e-6) return false;
+    const double f = 1.0 / det;
+    const d3 sv = o - a0;
+    const double u = f * dot(sv, hv);
+    if (u < 0.0 || u > 1.0) return false;
+    const d3 qv = cross(sv, e1);
+    const double v = f * dot(d, qv);
+    if (v < 0.0 || u + v > 1.0) return false;
+    t = f * dot(e2, qv);
+    return t > 1e-6;
+}
+
+// Conservative ray / box test (boxes are widened at build time, rt_bvh.cpp): false only when
+// no point of the box is on the ray at t >= 0.  tn = entry parameter (a lower bound).
+__device__ __forceinline__ bool bvh_box(const double* nd, d3 o, d3 d, d3 inv, double& tn) {
+    double lo = -INFINITY, hi = INFINITY;
+    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, ii[3] = {inv.x, inv.y, inv.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (dd[k] != 0.0) {
+            double t0 = (nd[k] - oo[k]) * ii[k], t1 = (nd[3 + k] - oo[k]) * ii[k];
+            if (t0 > t1) {
+                const double x = t0;
+                t0 = t1;
+                t1 = x;
+            }
+            lo = fmax(lo, t0);  // fmax/fmin drop a NaN operand: a NaN axis does not cull
+            hi = fmin(hi, t1);
+        } else if (oo[k] < nd[k] || oo[k] > nd[3 + k]) {
+            return false;
+        }
+    }
+    tn = lo;
+    return !(hi < 0.0) && !(lo > hi + 1e-12 * fabs(hi));
+}
+
+// The triangles' part of IntersectClosest over the BVH.  The reference tests triangles in index
+// order and replaces the running hit only when strictly closer, so among triangles it returns
+// the smallest t, and among equal smallest t the lowest index; the traversal keeps exactly that
+// (t, index) minimum, and a node is skipped only when its entry bound exceeds the current best
+// t by a 1e-9 margin (so a tie can never be skipped).  The merge with the sphere/plane result is
+// the reference's strict '<'.
+__device__ __forceinline__ void bvh_triangles(const double* tri, const double* bvh,
+                                              const int32_t* order, d3 o, d3 d, bool& found,
+                                              double& best, int& kind, int& idx) {
+    const d3 inv = mk(d.x != 0.0 ? 1.0 / d.x : 0.0, d.y != 0.0 ? 1.0 / d.y : 0.0,
+                      d.z != 0.0 ? 1.0 / d.z : 0.0);
+    bool tf = false;
+    double tb = 0.0;
+    int ti = 0;
+    int stk[kBvhStack];
+    int sp = 0;
+    double tn;
+    if (bvh_box(bvh, o, d, inv, tn)) stk[sp++] = 0;
+    while (sp > 0) {
+        const double* nd = bvh + kBvhNodeStride * stk[--sp];
+        const int first = __double2loint(nd[6]), count = __double2hiint(nd[6]);
+        if (count > 0) {
+            for (int j = first; j < first + count; ++j) {
+                const int i = order[j];
+                double t;
+                if (tri_hit(tri, i, o, d, t) && (!tf || t < tb || (t == tb && i < ti))) {
+                    tf = true;
+                    tb = t;
+                    ti = i;
+                }
+            }
+            continue;
+        }
+        const double bound = tf ? (found ? fmin(tb, best) : tb) : (found ? best : INFINITY);
+        const double lim = bound * (1.0 + 1e-9);
+        double t0, t1;
+        const bool h0 = bvh_box(bvh + kBvhNodeStride * first, o, d, inv, t0) && !(t0 > lim);
+        const bool h1 = bvh_box(bvh + kBvhNodeStride * (first + 1), o, d, inv, t1) && !(t1 > lim);
+        if (h0 && h1) {  // nearer child on top
+            const bool near0 = !(t1 < t0);
+            stk[sp++] = near0 ? first + 1 : first;
+            stk[sp++] = near0 ? first : first + 1;
+        } else if (h0) {
+            stk[sp++] = first;
+        } else if (h1) {
+            stk[sp++] = first + 1;
+        }
+    }
+    if (tf && (!found || tb < best)) {
+        found = true;
+        best = tb;
+        kind = 3;
+        idx = ti;
+    }
+}
 
 // Scene::IntersectClosest: spheres, then planes, then triangles; a later candidate replaces
 // the current one only when strictly closer (HitInfo::isCloserThan, Shape.h:36).
@@ -87,27 +190,17 @@ __device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) 
             }
         }
     }
-    for (int i = 0; i < S.nt; ++i) {
-        const double* q = S.tri + kTriStride * i;
-        const d3 a0 = mk(q[0], q[1], q[2]);
-        const d3 e1 = mk(q[3], q[4], q[5]);
-        const d3 e2 = mk(q[6], q[7], q[8]);
-        const d3 hv = cross(d, e2);
-        const double det = dot(e1, hv);
-        if (det > -1e-6 && det < 1e-6) continue;
-        const double f = 1.0 / det;
-        const d3 sv = o - a0;
-        const double u = f * dot(sv, hv);
-        if (u < 0.0 || u > 1.0) continue;
-        const d3 qv = cross(sv, e1);
-        const double v = f * dot(d, qv);
-        if (v < 0.0 || u + v > 1.0) continue;
-        const double t = f * dot(e2, qv);
-        if (t > 1e-6 && (!found || t < best)) {
-            found = true;
-            best = t;
-            kind = 3;
-            idx = i;
+    if (S.bvh) {
+        bvh_triangles(S.tri, S.bvh, S.bvh_tri, o, d, found, best, kind, idx);
+    } else {
+        for (int i = 0; i < S.nt; ++i) {
+            double t;
+            if (tri_hit(S.tri, i, o, d, t) && (!found || t < best)) {
+                found = true;
+                best = t;
+                kind = 3;
+                idx = i;
+            }
         }
     }
     h.t = best;
@@ -136,6 +229,8 @@ __device__ __forceinline__ SceneView stage_scene(const TraceParams& P, double* s
     S.sph_mat = P.sph_mat;
     S.pl_mat = P.pl_mat;
     S.tri_mat = P.tri_mat;
+    S.bvh = P.bvh;
+    S.bvh_tri = P.bvh_tri;
     if constexpr (LDS) {
         double* s_sph = smem;
         double* s_pl = s_sph + kSphStride * P.ns;
