@@ -11,7 +11,7 @@ from raytracingengine_amd import capi
 from raytracingengine_amd.configs import make_config
 
 CPU_SCALE = {"c1": 4, "c2": 4, "c3": 8, "c4": 16, "c5": 8, "mirror": 4, "glass": 4, "mesh": 4,
-             "c1_aa32": 10}
+             "c1_aa32": 10, "bigmesh": 8}
 
 
 def config(name, w=None, h=None):
@@ -23,7 +23,8 @@ threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
 ctx = capi.Context(0)
 s = torch.cuda.Stream(); ctx.set_stream(s.cuda_stream)
 rows = []
-names = sys.argv[1:] or ["c1", "c1_aa32", "c2", "c3", "c4", "c5", "mirror", "glass", "mesh"]
+names = sys.argv[1:] or ["c1", "c1_aa32", "c2", "c3", "c4", "c5", "mirror", "glass", "mesh",
+                          "bigmesh"]
 for name in names:
     sc = config(name)
     ds = ctx.scene(sc)
@@ -40,7 +41,8 @@ for name in names:
             ds.render_device(hdr.data_ptr(), None, ldr.data_ptr(), o)
         st = ctx.stats(); best = min(best, st.kernel_ms / st.launches)
     ds.close()
-    row = {"config": name, "resolution": [W, H], "aa": sc.camera.antiAliasingAmount, "spheres": len(sc.spheres),
+    row = {"config": name, "resolution": [W, H], "aa": sc.camera.antiAliasingAmount,
+           "triangles": len(sc.triangle_array()), "spheres": len(sc.spheres),
            "planes": len(sc.planes), "lights": len(sc.lights), "rays_per_frame": rays,
            "gpu_ms_per_frame": round(best, 4), "gpu_mrays_s": round(rays / best / 1e3, 1)}
     if po.ref_available():
