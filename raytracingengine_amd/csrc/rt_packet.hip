@@ -501,13 +501,35 @@ __device__ __forceinline__ int pk_occlusion(const PacketScene& S, const Masks<MA
     return undecided ? 2 : (blocked ? 1 : 0);
 }
 
+// Shadow-packet candidates: the origins `so` of the lanes in `casting_lanes` lie in a ball around
+// the first such lane's origin (exact), radius = the wave maximum of the distances in FP32
+// rounded up; every segment ends in the light's ball (lcenter, lrad); non-finite origins or
+// radius keep every sphere.
+template <int MAXC>
+__device__ __forceinline__ Masks<MAXC> shadow_masks(const PacketScene& S, bool casting_lane, d3 so,
+                                                    d3 lcenter, double lrad) {
+    const uint64_t casting = __ballot(casting_lane);
+    if (!casting) return all_candidates<MAXC>(S.ns);
+    const bool bad = casting_lane && !(isfinite(so.x) && isfinite(so.y) && isfinite(so.z));
+    const d3 c = lane_d3(so, __builtin_ctzll(casting));
+    float r_lane = 0.0f;
+    if (casting_lane) {  // |so − c| in FP32, rounded up (FP64 differences, 5e-7 rel. error)
+        const float dx = static_cast<float>(so.x - c.x), dy = static_cast<float>(so.y - c.y),
+                    dz = static_cast<float>(so.z - c.z);
+        r_lane = sqrtf(dot3f(dx, dy, dz, dx, dy, dz)) * (1.0f + 1e-5f);
+    }
+    const float R = wave_red<1>(r_lane);
+    return __ballot(bad) || !isfinite(R) ? all_candidates<MAXC>(S.ns)
+                                         : cull_capsule<MAXC>(S, c, R, lcenter, lrad);
+}
+
 // One light of directLightning (Scene.h:86-124) for the whole wave: every lane calls it
 // (uniform control flow for the packet reductions); `active` lanes shade.
 template <int MAXC, int FEAT, bool COUNT>
 __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P, d3 n, d3 view,
                                          const Hit& h, d3 lpos, d3 E, d3 lcenter, double lrad,
                                          double bias, int nchunks, d3& diff, d3& spec,
-                                         Counts& cnt) {
+                                         Counts& cnt, const Masks<MAXC>* pre = nullptr) {
     const d3 v = lpos - P;
     const double dist = length(v);
     const bool reach = active && !(dist <= 0.0);
@@ -515,22 +537,9 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     const double ndl = smax(0.0, dot(n, L));
     const bool need = reach && !(ndl <= 0.0) && !(dist <= bias);
     const d3 so = P + n * bias;
-    // packet bound: a ball around the first casting lane's origin (exact), radius = the
-    // wave maximum of the distances, rounded up to FP32
     const uint64_t casting = __ballot(need);
     if (!casting) return;  // no lane casts this shadow ray (uniform)
-    const bool bad = need && !(isfinite(so.x) && isfinite(so.y) && isfinite(so.z));
-    const d3 c = lane_d3(so, __builtin_ctzll(casting));
-    float r_lane = 0.0f;
-    if (need) {  // |so − c| in FP32, rounded up (FP64 differences, 5e-7 relative FP32 error)
-        const float dx = static_cast<float>(so.x - c.x), dy = static_cast<float>(so.y - c.y),
-                    dz = static_cast<float>(so.z - c.z);
-        r_lane = sqrtf(dot3f(dx, dy, dz, dx, dy, dz)) * (1.0f + 1e-5f);
-    }
-    const float R = wave_red<1>(r_lane);
-    const Masks<MAXC> M = __ballot(bad) || !isfinite(R)
-                              ? all_candidates<MAXC>(S.ns)
-                              : cull_capsule<MAXC>(S, c, R, lcenter, lrad);
+    const Masks<MAXC> M = pre ? *pre : shadow_masks<MAXC>(S, need, so, lcenter, lrad);
     if (!need) return;
     if (COUNT) cnt.shadow++;
     const int occ = pk_occlusion<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
@@ -677,6 +686,9 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
                     const d3 eu = mk(P.al_u[0], P.al_u[1], P.al_u[2]);
                     const d3 ev = mk(P.al_v[0], P.al_v[1], P.al_v[2]);
                     const d3 E = mk(P.al_E[0], P.al_E[1], P.al_E[2]);
+                    // one packet cull for all samples: every sample's casting lanes are hit
+                    // lanes with this origin, and every sample point is in (al_c, al_r)
+                    const Masks<MAXC> Ma = shadow_masks<MAXC>(S, hit, hp + n * bias, al_c, al_r);
                     for (int q = 0; q < P.al_samples; ++q) {
                         const double r1 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q));
                         const double r2 =
@@ -685,7 +697,7 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
                         const double fv = (static_cast<double>(q / P.al_k) + r2) / k;
                         const d3 lpos = (corner + eu * fu) + ev * fv;
                         pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, lpos, E, al_c, al_r,
-                                                    bias, nchunks, diff, spec, cnt);
+                                                    bias, nchunks, diff, spec, cnt, &Ma);
                     }
                 }
             }
