@@ -41,6 +41,10 @@ Vec3 reinhardJodie(const Vec3& color, double a);
 Vec3 uncharted2(const Vec3& color);
 Vec3 aces_approx(Vec3 v);
 
+// defined by the reference application file (compiled with main renamed, oracle/Makefile)
+Model LoadObject(const std::string& modelName, const Transform& transform,
+                 const Material& material);
+
 namespace {
 
 std::vector<double> read_f64(const char* path, size_t count) {
@@ -327,6 +331,23 @@ int mode_ppm(int argc, char** argv) {
     return 0;
 }
 
+// The reference application's OBJ import (RaytracingEngine.cpp:15-65, tinyobjloader): the
+// triangles of the loaded model, 9 doubles each (v0, v1, v2; identity transform).
+int mode_obj(int argc, char** argv) {
+    if (argc < 4) return 1;
+    const Model m = LoadObject(argv[2], Transform(), Material());
+    std::vector<double> out;
+    for (const Triangle& t : m.GetTrianglesFromModel(Material())) {
+        for (const Vec3& v : {t.tv0(), t.tv1(), t.tv2()}) {
+            out.push_back(v.x);
+            out.push_back(v.y);
+            out.push_back(v.z);
+        }
+    }
+    write_bytes(argv[3], out.data(), out.size() * sizeof(double));
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -342,6 +363,7 @@ int main(int argc, char** argv) {
     else if (m == "kat") rc = mode_kat(argc, argv);
     else if (m == "closest") rc = mode_closest(argc, argv);
     else if (m == "ppm") rc = mode_ppm(argc, argv);
+    else if (m == "obj") rc = mode_obj(argc, argv);
     if (rc == 1) std::fprintf(stderr, "bad arguments for mode %s\n", m.c_str());
     return rc;
 }

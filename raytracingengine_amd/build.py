@@ -75,7 +75,7 @@ def build_cpp_api(force: bool = False, verbose: bool = False) -> str:
     """The drop-in C++20 API (api/rtamd/*.cpp) as librtamd_cpp.so over librtamd.so, plus the
     example programs under examples/ (bin in examples/bin, rpath to the package dir)."""
     build_library(force=force, verbose=verbose)
-    srcs = [os.path.join(API_DIR, "rtamd", f) for f in ("scene.cpp", "image.cpp")]
+    srcs = [os.path.join(API_DIR, "rtamd", f) for f in ("scene.cpp", "image.cpp", "obj.cpp")]
     hdrs = [os.path.join(API_DIR, "rtamd", f) for f in os.listdir(os.path.join(API_DIR, "rtamd"))]
     link = [f"-L{HERE}", "-lrtamd", f"-Wl,-rpath,{HERE}", "-Wl,-rpath,$ORIGIN"]
     cxx = os.environ.get("CXX", "g++")

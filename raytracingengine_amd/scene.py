@@ -163,6 +163,11 @@ class SceneData:
     def add_triangle(self, v0, v1, v2, mat: Material, translation=(0.0, 0.0, 0.0)):
         self.triangles.append((tuple(v0), tuple(v1), tuple(v2), tuple(translation), mat))
 
+    def add_obj(self, path: str, translation=(0.0, 0.0, 0.0), mat: Material | None = None):
+        """A Model from a Wavefront OBJ file, as the reference application's LoadObject
+        (RaytracingEngine.cpp:15-65) builds it: see load_obj."""
+        self.add_model(load_obj(path), translation, mat if mat is not None else Material())
+
     def add_model(self, tris: Iterable, translation, mat: Material):
         self.models.append(([tuple(map(tuple, t)) for t in tris], tuple(translation), mat))
 
@@ -249,3 +254,99 @@ class SceneData:
     def write(self, path) -> None:
         with open(path, "w") as fh:
             fh.write(self.to_text())
+
+
+def tinyobj_real(s: str, fallback: float) -> float:
+    """A real as tinyobjloader v1.0.x reads it — the same restatement as tinyobj_real in
+    api/rtamd/obj.cpp (not correctly rounded; ".5" reads as the fallback)."""
+    lut = [1.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001]
+    i, n = 0, len(s)
+    if n == 0:
+        return fallback
+    sign = "+"
+    if s[0] in "+-":
+        sign = s[0]
+        i = 1
+    elif not s[0].isdigit():
+        return fallback
+    mantissa = 0.0
+    digits = 0
+    while i < n and s[i].isdigit():
+        mantissa *= 10
+        mantissa += int(s[i])
+        i += 1
+        digits += 1
+    if digits == 0:
+        return fallback
+    exponent = 0
+    if i < n and s[i] == ".":
+        i += 1
+        k = 1
+        while i < n and s[i].isdigit():
+            mantissa += int(s[i]) * (lut[k] if k < 8 else math.pow(10.0, -k))
+            k += 1
+            i += 1
+    if i < n and s[i] in "eE":
+        i += 1
+        esign = "+"
+        if i < n and s[i] in "+-":
+            esign = s[i]
+            i += 1
+        elif not (i < n and s[i].isdigit()):
+            return fallback
+        ed = 0
+        while i < n and s[i].isdigit():
+            exponent = exponent * 10 + int(s[i])
+            i += 1
+            ed += 1
+        if ed == 0:
+            return fallback
+        if esign == "-":
+            exponent = -exponent
+    val = math.ldexp(mantissa * math.pow(5.0, exponent), exponent) if exponent else mantissa
+    return val if sign == "+" else -val
+
+
+def load_obj(path: str) -> list[tuple[tuple[float, float, float], ...]]:
+    """Triangles of a Wavefront OBJ file as tinyobjloader v1.0.x (triangulate on) and the
+    reference's LoadObject produce them: `v` positions rounded to float32 (tinyobj's real_t) then
+    widened, `f` corners `i`, `i/t`, `i//n`, `i/t/n` (1-based; 0 read as 0; negative relative to
+    the vertices read so far) fanned from the first corner, faces in file order.  Same rules as
+    the C++ rtamd::LoadObject (api/rtamd/obj.cpp)."""
+    pos: list[tuple[float, float, float]] = []
+    tris = []
+
+    def atoi(tok: str) -> int:
+        digits = ""
+        for i, ch in enumerate(tok):
+            if ch.isdigit() or (i == 0 and ch in "+-"):
+                digits += ch
+            else:
+                break
+        try:
+            return int(digits)
+        except ValueError:
+            return 0
+
+    def f32(tok: str) -> float:
+        return float(np.float32(tinyobj_real(tok, 0.0)))
+
+    with open(path) as fh:
+        for line in fh:
+            parts = line.split()
+            if not parts:
+                continue
+            if parts[0] == "v":
+                xyz = (parts[1:4] + ["0", "0", "0"])[:3]
+                pos.append(tuple(f32(t) for t in xyz))
+            elif parts[0] == "f":
+                face = []
+                for tok in parts[1:]:
+                    i = atoi(tok)
+                    i = i - 1 if i > 0 else (0 if i == 0 else len(pos) + i)
+                    if not 0 <= i < len(pos):
+                        raise ValueError(f"OBJ face index out of range in {path}")
+                    face.append(i)
+                for k in range(2, len(face)):
+                    tris.append((pos[face[0]], pos[face[k - 1]], pos[face[k]]))
+    return tris

@@ -212,8 +212,23 @@ def main():
     print(json.dumps(sizes))
 
 
+def obj_golden():
+    """The reference application's LoadObject (tinyobjloader) on the OBJ fixtures: triangles as
+    9 doubles each (oracle/_ref/ref_harness obj)."""
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for name in ("objtest", "box"):
+            dst = os.path.join(td, name + ".f64")
+            run("obj", os.path.join(HERE, name + ".obj"), dst)
+            out[name] = np.fromfile(dst, np.float64).reshape(-1, 9)
+    np.savez_compressed(os.path.join(HERE, "obj_tris.npz"), **out)
+    print({k: v.shape for k, v in out.items()})
+
+
 if __name__ == "__main__":
     if "--refapp" in sys.argv:
         refapp_golden()
+    elif "--obj" in sys.argv:
+        obj_golden()
     else:
         main()
