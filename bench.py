@@ -48,8 +48,10 @@ def parse_args(argv=None):
                     help="HDR framebuffer type: f64 = the reference's std::vector<Vec3> (default)")
     ap.add_argument("--event-every", type=int, default=10,
                     help="bracket every n-th timed launch with HIP events (0: none)")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="frames in flight for the extra 'pipelined' measurement (1: skip)")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="> 1: also measure K frames with this many in flight on as many "
+                         "streams ('pipelined' field; off by default so that a rocprofv3 "
+                         "summary of the default command is the headline's launches only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=6,
                     help="reference frames timed for cpu_baseline (first one is warm-up)")

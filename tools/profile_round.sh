@@ -8,6 +8,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
+timeout -k 10 300 python bench.py --no-cpu-baseline --inflight 2 > $OUT/bench_pipelined.json 2>> $OUT/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 bench.py --no-cpu-baseline --steps 200 > $OUT/bench_prof.json 2> $OUT/prof.err
 for grp in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc/p_$grp -o pmc -- python3 tools/profile_kernel.py c2 20 > $OUT/pmc_$grp.log 2>&1
