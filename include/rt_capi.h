@@ -204,6 +204,16 @@ rt_status rt_render(rt_context* ctx, const rt_scene* scene, const rt_camera* cam
                     const rt_render_opts* opts, double* hdr64_out, float* hdr32_out,
                     uint8_t* ldr_out, rt_stats* stats);
 
+/* One frame on n contexts (one per GPU, each with its own copy of the scene: scenes[i] belongs to
+ * ctxs[i]), assembled in the caller's host buffers — Scene::RenderImage over the GPUs of a node
+ * from one process.  Context i renders the block-cyclic row set i of n (opts->row_block rows per
+ * block, default 16; the row range and row_cycle of opts must be left at the whole image); all
+ * contexts run concurrently, then every context's rows are copied to their image rows.  Stats,
+ * when requested, are summed over the contexts. */
+rt_status rt_render_multi(rt_context* const* ctxs, rt_scene* const* scenes, int n,
+                          const rt_camera* cam, const rt_render_opts* opts, double* hdr64_out,
+                          float* hdr32_out, uint8_t* rgb8_out, rt_stats* stats);
+
 /* Asynchronous render into DEVICE buffers on the context's stream (inputs and outputs stay
  * resident in HBM).  Same layouts as rt_render; pointers are device pointers or NULL. */
 rt_status rt_render_device(rt_context* ctx, const rt_scene* scene, const rt_camera* cam,

@@ -88,11 +88,16 @@ rt_render_opts Scene::optsDesc(int tonemap) const {
 }
 
 rt_scene* Scene::upload() const {
-    using namespace rtamd;
     if (dev_ && dev_->version == version_ && dev_->device == device_) return dev_->scene;
+    dev_ = uploadTo(device_);
+    return dev_->scene;
+}
+
+std::shared_ptr<rtamd::SceneDevice> Scene::uploadTo(int device) const {
+    using namespace rtamd;
     auto sd = std::make_shared<SceneDevice>();
-    sd->device = device_;
-    sd->ctx = thread_context(device_);
+    sd->device = device;
+    sd->ctx = thread_context(device);
 
     std::vector<rt_sphere> sp(spheres.size());
     for (size_t i = 0; i < spheres.size(); ++i) {
@@ -142,15 +147,33 @@ rt_scene* Scene::upload() const {
     check(rt_scene_create(sd->ctx, &d, &sd->scene), "rt_scene_create");
     if (areaLight_) check(rt_scene_set_area_light(sd->scene, &*areaLight_), "rt_scene_set_area_light");
     sd->version = version_;
-    dev_ = sd;
-    return sd->scene;
+    return sd;
+}
+
+bool Scene::renderMulti(const rt_render_opts& o, double* h64, float* h32, uint8_t* h8) const {
+    if (devices_.size() < 2) return false;
+    if (multi_.size() != devices_.size()) multi_.assign(devices_.size(), nullptr);
+    std::vector<rt_context*> ctxs;
+    std::vector<rt_scene*> scs;
+    for (size_t i = 0; i < devices_.size(); ++i) {
+        if (!multi_[i] || multi_[i]->version != version_ || multi_[i]->device != devices_[i])
+            multi_[i] = uploadTo(devices_[i]);
+        ctxs.push_back(multi_[i]->ctx);
+        scs.push_back(multi_[i]->scene);
+    }
+    const rt_camera cam = cameraDesc();
+    rtamd::check(rt_render_multi(ctxs.data(), scs.data(), static_cast<int>(ctxs.size()), &cam,
+                                 &o, h64, h32, h8, countRays_ ? &lastStats_ : nullptr),
+                 "rt_render_multi");
+    return true;
 }
 
 std::vector<Vec3> Scene::RenderImage() const {
-    rt_scene* sc = upload();
-    const rt_camera cam = cameraDesc();
     const rt_render_opts o = optsDesc(RT_TONEMAP_NONE);
     std::vector<Vec3> img(camera.width * camera.height, Vec3(0, 0, 0));
+    if (renderMulti(o, reinterpret_cast<double*>(img.data()), nullptr, nullptr)) return img;
+    rt_scene* sc = upload();
+    const rt_camera cam = cameraDesc();
     // Vec3 is three packed doubles: the device writes the reference's vector<Vec3> layout.
     rtamd::check(rt_render(dev_->ctx, sc, &cam, &o, reinterpret_cast<double*>(img.data()), nullptr,
                            nullptr, countRays_ ? &lastStats_ : nullptr),
@@ -159,10 +182,11 @@ std::vector<Vec3> Scene::RenderImage() const {
 }
 
 std::vector<Color> Scene::RenderImageTonemapped(int op) const {
-    rt_scene* sc = upload();
-    const rt_camera cam = cameraDesc();
     const rt_render_opts o = optsDesc(op);
     std::vector<Color> img(camera.width * camera.height);
+    if (renderMulti(o, nullptr, nullptr, reinterpret_cast<uint8_t*>(img.data()))) return img;
+    rt_scene* sc = upload();
+    const rt_camera cam = cameraDesc();
     rtamd::check(rt_render(dev_->ctx, sc, &cam, &o, nullptr, nullptr,
                            reinterpret_cast<uint8_t*>(img.data()), countRays_ ? &lastStats_ : nullptr),
                  "rt_render");
@@ -170,10 +194,11 @@ std::vector<Color> Scene::RenderImageTonemapped(int op) const {
 }
 
 std::vector<float> Scene::RenderImageF32() const {
-    rt_scene* sc = upload();
-    const rt_camera cam = cameraDesc();
     const rt_render_opts o = optsDesc(RT_TONEMAP_NONE);
     std::vector<float> img(camera.width * camera.height * 3);
+    if (renderMulti(o, nullptr, img.data(), nullptr)) return img;
+    rt_scene* sc = upload();
+    const rt_camera cam = cameraDesc();
     rtamd::check(rt_render(dev_->ctx, sc, &cam, &o, nullptr, img.data(), nullptr, countRays_ ? &lastStats_ : nullptr),
                  "rt_render");
     return img;

@@ -50,7 +50,12 @@ class Scene {
     mutable rt_stats lastStats_{};
     bool countRays_ = false;
 
+    std::vector<int> devices_;  // > 1 entries: RenderImage over these GPUs (rt_render_multi)
+    mutable std::vector<std::shared_ptr<rtamd::SceneDevice>> multi_;
+
     rt_scene* upload() const;
+    std::shared_ptr<rtamd::SceneDevice> uploadTo(int device) const;
+    bool renderMulti(const rt_render_opts& o, double* h64, float* h32, uint8_t* h8) const;
     rt_camera cameraDesc() const;
     rt_render_opts optsDesc(int tonemap) const;
     void touch() { ++version_; }
@@ -78,7 +83,11 @@ public:
     std::vector<Color> RenderImageTonemapped(int op = RT_TONEMAP_ACES) const;
     // float32 HDR framebuffer (12 B/px) instead of the reference's FP64 Vec3 (24 B/px).
     std::vector<float> RenderImageF32() const;
-    void SetDevice(int device) { device_ = device; dev_.reset(); }
+    void SetDevice(int device) { device_ = device; dev_.reset(); devices_.clear(); }
+    // RenderImage / RenderImageTonemapped / RenderImageF32 over several GPUs of the node from
+    // this process: one scene copy per GPU, block-cyclic rows, assembled on the host (distinct
+    // device ids: one context per device and thread)
+    void SetDevices(const std::vector<int>& devices) { devices_ = devices; multi_.clear(); }
     void SetMaxRecursion(int depth) { maxRecursion = depth; }
     // build-defined area light (BASELINE config 5); nullopt removes it
     void SetAreaLight(const std::optional<rt_area_light>& light) { areaLight_ = light; touch(); }

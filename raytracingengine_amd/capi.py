@@ -34,6 +34,7 @@ EXPORTED = [
     "rt_last_error", "rt_device_count", "rt_render_opts_default", "rt_context_create",
     "rt_context_destroy", "rt_context_set_stream", "rt_context_synchronize", "rt_scene_create",
     "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
+    "rt_render_multi",
     "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
     "rt_debug_f64_ops",
 ]
@@ -104,6 +105,7 @@ def load_library(path: str = LIB_PATH):
         "rt_scene_set_area_light": [vp, vp],
         "rt_render": [vp, vp, vp, vp, vp, vp, vp, vp],
         "rt_render_device": [vp, vp, vp, vp, vp, vp, vp],
+        "rt_render_multi": [vp, vp, i32, vp, vp, vp, vp, vp, vp],
         "rt_stats_read": [vp, vp],
         "rt_stats_reset": [vp],
         "rt_trace_rays": [vp, vp, vp, vp, ctypes.c_size_t, vp, vp],
@@ -294,3 +296,30 @@ class DeviceScene:
         """Asynchronous render into device pointers (rt_render_device)."""
         _check(_lib.rt_render_device(self.ctx.handle, self._h, self.camera.ctypes.data,
                                      ctypes.byref(opts), d_hdr64, d_hdr32, d_ldr))
+
+
+def render_multi(scenes: list, *, hdr64=True, tonemap: int = TONEMAP_NONE, stats=False,
+                 row_block: int = 0, **opt_kw) -> dict:
+    """One frame over several contexts (rt_render_multi): `scenes` are DeviceScenes of the same
+    SceneData, one per context; block-cyclic rows, assembled on the host."""
+    L = load_library()
+    n = len(scenes)
+    cam = scenes[0].data.camera
+    o = default_opts(tonemap=tonemap, row_block=row_block, **opt_kw)
+    ctxs = (ctypes.c_void_p * n)(*[ds.ctx.handle for ds in scenes])
+    scs = (ctypes.c_void_p * n)(*[ds._h for ds in scenes])
+    a64 = np.empty((cam.height, cam.width, 3), np.float64) if hdr64 else None
+    ldr = np.empty((cam.height, cam.width, 3), np.uint8) if tonemap != TONEMAP_NONE else None
+    st = Stats()
+    _check(L.rt_render_multi(ctxs, scs, n, scenes[0].camera.ctypes.data, ctypes.byref(o),
+                             a64.ctypes.data if a64 is not None else None, None,
+                             ldr.ctypes.data if ldr is not None else None,
+                             ctypes.byref(st) if stats else None))
+    out = {}
+    if a64 is not None:
+        out["hdr64"] = a64
+    if ldr is not None:
+        out["ldr"] = ldr
+    if stats:
+        out["trace_rays"], out["shadow_rays"] = st.trace_rays, st.shadow_rays
+    return out

@@ -628,6 +628,95 @@ rt_status rt_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
     return RT_OK;
 }
 
+rt_status rt_render_multi(rt_context* const* ctxs, rt_scene* const* scenes, int n,
+                          const rt_camera* cam, const rt_render_opts* opts, double* h64,
+                          float* h32, uint8_t* hldr, rt_stats* stats) {
+    if (n < 1 || !ctxs || !scenes) return fail(RT_ERR_INVALID_ARG, "rt_render_multi: n < 1 or NULL");
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i] || !scenes[i] || scenes[i]->ctx != ctxs[i])
+            return fail(RT_ERR_INVALID_ARG, "rt_render_multi: scene " + std::to_string(i) +
+                                                " missing or not of context " + std::to_string(i));
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i])  // each context renders into its own buffers
+                return fail(RT_ERR_INVALID_ARG, "rt_render_multi: context repeated");
+    }
+    rt_status st = validate_camera(cam);
+    if (st != RT_OK) return st;
+    rt_render_opts base;
+    if (opts) base = *opts;
+    else rt_render_opts_default(&base);
+    if (base.row_begin != 0 || (base.row_end != 0 && base.row_end != cam->height) ||
+        base.row_cycle > 1)
+        return fail(RT_ERR_INVALID_ARG, "rt_render_multi renders the whole image; the row "
+                                        "split is its own (row_block only)");
+    if (stats) base.flags |= RT_FLAG_COUNT_RAYS;
+    const uint32_t H = cam->height, W = cam->width;
+    const uint32_t block = n == 1 ? 0 : (base.row_block ? base.row_block : 16);
+    std::vector<rt_render_opts> o(static_cast<size_t>(n), base);
+    std::vector<uint32_t> rows(static_cast<size_t>(n));
+    // 1. every context renders its rows (block-cyclic) into its own device buffers, async
+    for (int i = 0; i < n; ++i) {
+        rt_context* ctx = ctxs[i];
+        DeviceGuard g(ctx->device);
+        o[i].row_end = H;
+        if (block) {
+            o[i].row_begin = static_cast<uint32_t>(i) * block;
+            o[i].row_block = static_cast<uint16_t>(block);
+            o[i].row_cycle = static_cast<uint16_t>(n);
+            if (o[i].row_begin >= H) {
+                rows[i] = 0;
+                continue;
+            }
+        }
+        rows[i] = rendered_rows(o[i], H);
+        const size_t npx = static_cast<size_t>(rows[i]) * W;
+        if (h64) RT_HIP(ctx->out64.ensure(npx * 3 * sizeof(double)));
+        if (h32) RT_HIP(ctx->out32.ensure(npx * 3 * sizeof(float)));
+        if (hldr) RT_HIP(ctx->ldr.ensure(npx * 3));
+        if (stats)
+            RT_HIP(hipMemsetAsync(ctx->counters.ptr, 0, 2 * sizeof(unsigned long long),
+                                  ctx->stream));
+        st = enqueue(ctx, scenes[i], cam, &o[i],
+                     h64 ? static_cast<double*>(ctx->out64.ptr) : nullptr,
+                     h32 ? static_cast<float*>(ctx->out32.ptr) : nullptr,
+                     hldr ? static_cast<uint8_t*>(ctx->ldr.ptr) : nullptr);
+        if (st != RT_OK) return st;
+    }
+    // 2. gather: each context's packed rows back to their image rows in the caller's buffers
+    if (stats) std::memset(stats, 0, sizeof *stats);
+    for (int i = 0; i < n; ++i) {
+        if (rows[i] == 0) continue;
+        rt_context* ctx = ctxs[i];
+        DeviceGuard g(ctx->device);
+        const size_t row64 = size_t(W) * 3 * sizeof(double), row32 = size_t(W) * 3 * sizeof(float),
+                     row8 = size_t(W) * 3;
+        uint32_t k = 0;  // packed row of this context
+        for (uint32_t b0 = o[i].row_begin; b0 < H; b0 += block ? block * n : H) {
+            const uint32_t nb = block ? std::min(block, H - b0) : rows[i];
+            if (h64)
+                RT_HIP(hipMemcpyAsync(reinterpret_cast<char*>(h64) + b0 * row64,
+                                      static_cast<char*>(ctx->out64.ptr) + k * row64, nb * row64,
+                                      hipMemcpyDeviceToHost, ctx->stream));
+            if (h32)
+                RT_HIP(hipMemcpyAsync(reinterpret_cast<char*>(h32) + b0 * row32,
+                                      static_cast<char*>(ctx->out32.ptr) + k * row32, nb * row32,
+                                      hipMemcpyDeviceToHost, ctx->stream));
+            if (hldr)
+                RT_HIP(hipMemcpyAsync(hldr + b0 * row8, static_cast<char*>(ctx->ldr.ptr) + k * row8,
+                                      nb * row8, hipMemcpyDeviceToHost, ctx->stream));
+            k += nb;
+        }
+        RT_HIP(hipStreamSynchronize(ctx->stream));
+        if (stats) {
+            unsigned long long c[2] = {0, 0};
+            RT_HIP(hipMemcpy(c, ctx->counters.ptr, sizeof c, hipMemcpyDeviceToHost));
+            stats->trace_rays += c[0];
+            stats->shadow_rays += c[1];
+        }
+    }
+    return RT_OK;
+}
+
 rt_status rt_stats_read(rt_context* ctx, rt_stats* out) {
     if (!ctx || !out) return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_stats_read");
     DeviceGuard g(ctx->device);

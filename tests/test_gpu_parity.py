@@ -409,3 +409,26 @@ def test_bvh_ties_go_to_lowest_index(ctx):
     b = _render(ctx, scene(False), hdr64=True)
     assert len(scene(True).triangle_array()) >= 256
     assert np.array_equal(a["hdr64"], b["hdr64"])
+
+
+# ------------------------------------------------------------------ one frame, several contexts
+@pytest.mark.parametrize("name,n,block", [("c2", 3, 16), ("glass", 2, 0), ("c3", 4, 7)])
+def test_render_multi_equals_single(name, n, block):
+    """rt_render_multi (Scene::SetDevices): n contexts — here all on GPU 0 — render their
+    block-cyclic rows concurrently and the host assembles one frame equal to the single-context
+    render, ray counts summed."""
+    sc = make_config(name, 240, 136)
+    ctxs = [capi.Context(0) for _ in range(n)]
+    try:
+        scenes = [c.scene(sc) for c in ctxs]
+        multi = capi.render_multi(scenes, hdr64=True, tonemap=1, stats=True, row_block=block)
+        single = scenes[0].render(hdr64=True, tonemap=1, stats=True)
+        for ds in scenes:
+            ds.close()
+    finally:
+        for c in ctxs:
+            c.close()
+    assert np.array_equal(multi["hdr64"], single["hdr64"])
+    assert np.array_equal(multi["ldr"], single["ldr"])
+    assert (multi["trace_rays"], multi["shadow_rays"]) == (single["trace_rays"],
+                                                            single["shadow_rays"])
