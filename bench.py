@@ -91,6 +91,15 @@ def cpu_baseline(sc, rays_per_frame: int, frames: int):
         used, kind = threads, "port"
     timed = sorted(ms[1:] if len(ms) > 1 else ms)
     med = timed[len(timed) // 2]
+    # SURVEY §8d also asks for the one-core figure: one frame after the warm-up above
+    if po.ref_available():
+        _, ms1, _ = po.ref_render(sc, repeat=1, threads=1, want_image=False)
+    else:
+        t0 = time.perf_counter()
+        po.render(sc, nthreads=1)
+        ms1 = [(time.perf_counter() - t0) * 1e3]
+    single = {"value": rays_per_frame / (ms1[0] / 1e3) / 1e6, "cores": 1,
+              "ms_per_frame": ms1[0]}
     return {
         "value": rays_per_frame / (med / 1e3) / 1e6,
         "unit": "Mrays/s",
@@ -100,6 +109,7 @@ def cpu_baseline(sc, rays_per_frame: int, frames: int):
                   f"{sc.name} (Scene::RenderImage only, first frame warm-up; median "
                   f"{med:.1f} ms/frame)",
         "ms_per_frame": med,
+        "single_core": single,
     }
 
 
