@@ -247,6 +247,11 @@ rt_status rt_tonemap(rt_context* ctx, const double* hdr, size_t n_pixels, int op
 rt_status rt_debug_f64_ops(rt_context* ctx, const double* x, const double* y, size_t n,
                            double* out);
 
+/* Test hook: per 3-vector v (3*n doubles), the normalize / light-vector results of the fast
+ * sqrt/division cores next to the compiler's exact lowering, so the parity suite can pin them bit
+ * for bit.  out: 16*n doubles (layout in rt_trace.hip, debug_vec_kernel). */
+rt_status rt_debug_vec_ops(rt_context* ctx, const double* v, size_t n, double* out);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

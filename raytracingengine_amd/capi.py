@@ -36,7 +36,7 @@ EXPORTED = [
     "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
     "rt_render_multi",
     "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
-    "rt_debug_f64_ops",
+    "rt_debug_f64_ops", "rt_debug_vec_ops",
 ]
 
 
@@ -112,6 +112,7 @@ def load_library(path: str = LIB_PATH):
         "rt_intersect_rays": [vp, vp, vp, ctypes.c_size_t, vp],
         "rt_tonemap": [vp, vp, ctypes.c_size_t, i32, vp],
         "rt_debug_f64_ops": [vp, vp, vp, ctypes.c_size_t, vp],
+        "rt_debug_vec_ops": [vp, vp, ctypes.c_size_t, vp],
     }.items():
         fn = getattr(L, name)
         fn.argtypes = args
@@ -209,6 +210,12 @@ class Context:
         out = np.empty((x.size, 4), np.float64)
         _check(_lib.rt_debug_f64_ops(self._h, x.ctypes.data, y.ctypes.data, x.size,
                                      out.ctypes.data))
+        return out
+
+    def debug_vec_ops(self, v: np.ndarray) -> np.ndarray:
+        v = np.ascontiguousarray(v, np.float64).reshape(-1, 3)
+        out = np.empty((v.shape[0], 16), np.float64)
+        _check(_lib.rt_debug_vec_ops(self._h, v.ctypes.data, v.shape[0], out.ctypes.data))
         return out
 
 

@@ -853,4 +853,17 @@ rt_status rt_debug_f64_ops(rt_context* ctx, const double* x, const double* y, si
     return RT_OK;
 }
 
+rt_status rt_debug_vec_ops(rt_context* ctx, const double* v, size_t n, double* out) {
+    if (!ctx || !v || !out) return fail(RT_ERR_INVALID_ARG, "NULL argument");
+    DeviceGuard g(ctx->device);
+    RT_HIP(ctx->dbg.ensure(n * 19 * sizeof(double)));
+    double* dv = static_cast<double*>(ctx->dbg.ptr);
+    double* dout = dv + 3 * n;
+    RT_HIP(hipMemcpyAsync(dv, v, 3 * n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    RT_HIP(launch_debug_vec(dv, n, dout, ctx->stream));
+    RT_HIP(hipMemcpyAsync(out, dout, 16 * n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
 }  // extern "C"

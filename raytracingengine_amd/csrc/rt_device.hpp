@@ -34,14 +34,107 @@ __device__ __forceinline__ d3 cross(d3 a, d3 b) {
     return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
 __device__ __forceinline__ double length(d3 a) { return sqrt(dot(a, a)); }
+
+// ------------------------------------------------------------------ exact sqrt / division cores
+// gfx950 lowers the correctly rounded FP64 sqrt and division to Newton-Raphson cores wrapped in
+// range scaling and special-case fix-ups:
+//   sqrt(x): x < 2^-767 ? scale by 2^256; v_rsq r; g = x·r; h = r·0.5; e = fma(−h, g, 0.5);
+//            g = fma(g, e, g); h = fma(h, e, h); 2× { e = fma(−g, g, x); g = fma(e, h, g) };
+//            unscale by 2^-128; x ∈ {±0, +inf} ? x : g                       (17 VALU)
+//   n / d:   v_div_scale (d), v_div_scale (n); v_rcp r; 2× { e = fma(−d, r, 1); r = fma(r, e, r) };
+//            q = n·r; e = fma(−d, q, n); v_div_fmas(e, r, q); v_div_fixup       (11 VALU)
+// For operands inside the ranges below every scale step is the identity (v_div_scale returns
+// its operand with VCC = 0, so v_div_fmas is a plain FMA) and every fix-up returns the core's
+// value, so the cores alone are the same instructions on the same values: the same bits, in
+// 10 and 8 VALU.  The reciprocal refinement depends on d only, so a vector divided by one
+// scalar shares it (3 VALU per further component).  Ranges (V_DIV_SCALE_F64 scales when
+// exp(n) ≤ 53 biased, i.e. |n| < 2^-969, when d or 1/d or n/d is subnormal, or when
+// exp(n) − exp(d) ≥ 768; the sqrt lowering scales below 2^-767):
+//   sqrt_core(x):          finite x ≥ 2^-767
+//   div_core(n, d, r(d)):  2^-900 ≤ |n|, 2^-400 ≤ |d| ≤ 2^400, |n/d| ≥ 2^-1000, all finite
+// Every caller checks its operands and takes the compiler's exact lowering otherwise; the
+// equality is pinned bit for bit by tests/test_gpu_parity.py::test_fast_exact_cores.
+__device__ __forceinline__ double sqrt_core(double x) {
+    double r = __builtin_amdgcn_rsq(x);
+    double g = x * r;
+    double h = r * 0.5;
+    const double e = fma(-h, g, 0.5);
+    g = fma(g, e, g);
+    h = fma(h, e, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    g = fma(d, h, g);
+    return g;
+}
+__device__ __forceinline__ double rcp_refined(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    return r;
+}
+__device__ __forceinline__ double div_core(double n, double d, double r) {
+    const double q = n * r;
+    const double e = fma(-d, q, n);
+    return fma(e, r, q);
+}
+// sqrt(dot(a, a)) with the dot product in the normalize range [2^-78, 2^120]: the length is in
+// [2^-39, 2^60] (> 1e-12), and components with |c| ≥ 2^-900 divide by it exactly in div_core.
+constexpr double kUnitLo = 0x1p-78, kUnitHi = 0x1p120, kNumLo = 0x1p-900;
+__device__ __forceinline__ bool unit_fast_ok(d3 a, double x) {
+    return x >= kUnitLo && x <= kUnitHi && fabs(a.x) >= kNumLo && fabs(a.y) >= kNumLo &&
+           fabs(a.z) >= kNumLo;
+}
+
 // Vec3::normalize: zero vector below 1e-12, otherwise three true divisions.
 // x / 1.0 == x exactly (IEEE), so an already-unit vector skips its three divisions.
-__device__ __forceinline__ d3 unit(d3 a) {
+__device__ __forceinline__ d3 unit_exact(d3 a) {
     const double l = length(a);
     if (l <= 1e-12) return {0.0, 0.0, 0.0};
     if (l == 1.0) return a;
     return sdiv(a, l);
 }
+// The same bits through the cores when the operands allow it (zero components, e.g. axis-
+// aligned normals, take the exact path unless the length is exactly 1).
+__device__ __forceinline__ d3 unit(d3 a) {
+    const double x = dot(a, a);
+    d3 out;
+    if (x >= kUnitLo && x <= kUnitHi) {
+        const double l = sqrt_core(x);
+        if (l == 1.0) {
+            out = a;
+        } else if (fabs(a.x) >= kNumLo && fabs(a.y) >= kNumLo && fabs(a.z) >= kNumLo) {
+            const double r = rcp_refined(l);
+            out = mk(div_core(a.x, l, r), div_core(a.y, l, r), div_core(a.z, l, r));
+        } else {
+            out = sdiv(a, l);
+        }
+    } else {
+        const double l = sqrt(x);
+        out = l <= 1e-12 ? mk(0.0, 0.0, 0.0) : (l == 1.0 ? a : sdiv(a, l));
+    }
+    return out;
+}
+// directLightning's light vector (Scene.h:87-90, 110): dist = v.length(), L = v / dist and
+// 1 / (dist·dist), through the cores when the operands allow it.  L is only meaningful for
+// dist > 0 (the reference skips the light otherwise).
+__device__ __forceinline__ void light_dir(d3 v, double& dist, d3& L, double& inv_d2) {
+    const double x = dot(v, v);
+    if (unit_fast_ok(v, x)) {
+        dist = sqrt_core(x);
+        const double r = rcp_refined(dist);
+        L = mk(div_core(v.x, dist, r), div_core(v.y, dist, r), div_core(v.z, dist, r));
+        const double dd = dist * dist;  // in [2^-78, 2^120]
+        inv_d2 = div_core(1.0, dd, rcp_refined(dd));
+    } else {
+        dist = sqrt(x);
+        L = sdiv(v, dist);
+        inv_d2 = 1.0 / (dist * dist);
+    }
+}
+
 // std::max / std::min / std::clamp with libstdc++'s comparison order (NaN handling).
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
 __device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }
@@ -67,11 +160,16 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
+__device__ __forceinline__ uint64_t pixel_key(uint64_t seed, uint64_t pixel) {
+    return mix64(seed ^ (0x9E3779B97F4A7C15ULL * (pixel + 1ULL)));
+}
+__device__ __forceinline__ double u01_key(uint64_t key, uint32_t stream, uint32_t index) {
+    const uint64_t h = mix64(key ^ ((static_cast<uint64_t>(stream) << 32) | index));
+    return static_cast<double>(h >> 11) * 0x1.0p-53;
+}
 __device__ __forceinline__ double u01(uint64_t seed, uint64_t pixel, uint32_t stream,
                                       uint32_t index) {
-    uint64_t h = mix64(seed ^ (0x9E3779B97F4A7C15ULL * (pixel + 1ULL)));
-    h = mix64(h ^ ((static_cast<uint64_t>(stream) << 32) | index));
-    return static_cast<double>(h >> 11) * 0x1.0p-53;
+    return u01_key(pixel_key(seed, pixel), stream, index);
 }
 
 // Sky colour, Scene::backgroundColor (Scene.h:30-33).

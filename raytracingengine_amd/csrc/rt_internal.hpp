@@ -94,5 +94,6 @@ hipError_t launch_intersect_rays(const TraceParams& p, const double* rays, size_
 hipError_t launch_tonemap(const double* hdr, size_t n, int op, uint8_t* out, hipStream_t stream);
 hipError_t launch_debug_f64(const double* x, const double* y, size_t n, double* out,
                             hipStream_t stream);
+hipError_t launch_debug_vec(const double* v, size_t n, double* out, hipStream_t stream);
 
 }  // namespace rtamd

@@ -243,6 +243,39 @@ __device__ __forceinline__ void sphere_roots(double b, double disc, double two_a
     }
 }
 
+// sphere_roots through the sqrt/division cores (rt_device.hpp), r2a = rcp_refined(two_a) with
+// two_a in [2^-100, 2^100].  A finite disc ≥ 2^-767 keeps b, √disc and both numerators finite;
+// a numerator |n| ≥ 2^-900 divides exactly, and a smaller one gives |t| < 2^-790 both exactly
+// and through the core, so the 1e-6 test (the only use of such a root) decides alike.  Other
+// discriminants take the literal path.  t0 ≤ t1 as in sphere_roots.
+__device__ __forceinline__ void sphere_roots_core(double b, double disc, double two_a, double r2a,
+                                                  int i, bool& found, double& best, int& kind,
+                                                  int& idx) {
+    if (disc < 0.0) return;
+    double t;
+    if (disc >= 0x1p-767 && disc <= 0x1.fffffffffffffp+1023) {
+        const double sq = sqrt_core(disc);
+        t = div_core(-b - sq, two_a, r2a);
+        if (t < 1e-6) {
+            t = div_core(-b + sq, two_a, r2a);
+            if (t < 1e-6) return;
+        }
+    } else {
+        const double sq = sqrt(disc);
+        t = (-b - sq) / two_a;
+        if (t < 1e-6) {
+            t = (-b + sq) / two_a;
+            if (t < 1e-6) return;
+        }
+    }
+    if (!found || t < best) {
+        found = true;
+        best = t;
+        kind = 1;
+        idx = i;
+    }
+}
+
 // The reference's literal root selection, for degenerate directions (2a not > 0).
 __device__ __forceinline__ void sphere_roots_literal(double b, double disc, double two_a, int i,
                                                      bool& found, double& best, int& kind,
@@ -315,18 +348,36 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
     const double a = dot(d, d);
     const double two_a = 2.0 * a, four_a = 4.0 * a;
     const bool regular = two_a > 0.0;
+    const bool core = two_a >= 0x1p-100 && two_a <= 0x1p100;  // camera rays are unit vectors
+    if (__ballot(!core) == 0) {  // uniform: the whole wave divides through the shared reciprocal
+        const double r2a = rcp_refined(two_a);
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-        if (c >= nchunks) break;
-        uint64_t m = M.m[c];
-        while (m) {
-            const int i = c * 64 + __builtin_ctzll(m);
-            m &= m - 1;
-            const double* q = S.pre + 4 * i;
-            const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
-            const double disc = b * b - four_a * q[3];
-            if (regular) sphere_roots(b, disc, two_a, i, found, best, kind, idx);
-            else sphere_roots_literal(b, disc, two_a, i, found, best, kind, idx);
+        for (int c = 0; c < MAXC; ++c) {
+            if (c >= nchunks) break;
+            uint64_t m = M.m[c];
+            while (m) {
+                const int i = c * 64 + __builtin_ctzll(m);
+                m &= m - 1;
+                const double* q = S.pre + 4 * i;
+                const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
+                const double disc = b * b - four_a * q[3];
+                sphere_roots_core(b, disc, two_a, r2a, i, found, best, kind, idx);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            if (c >= nchunks) break;
+            uint64_t m = M.m[c];
+            while (m) {
+                const int i = c * 64 + __builtin_ctzll(m);
+                m &= m - 1;
+                const double* q = S.pre + 4 * i;
+                const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
+                const double disc = b * b - four_a * q[3];
+                if (regular) sphere_roots(b, disc, two_a, i, found, best, kind, idx);
+                else sphere_roots_literal(b, disc, two_a, i, found, best, kind, idx);
+            }
         }
     }
     for (int i = 0; i < S.np; ++i) {
@@ -441,8 +492,8 @@ __device__ __forceinline__ int pk_occlusion(const PacketScene& S, const Masks<MA
     if constexpr ((FEAT & kFeatTris) != 0) return 2;
     const double a = dot(d, d);
     const double two_a = 2.0 * a, four_a = 4.0 * a;
-    if (!(two_a > 0.0)) return 2;
-    const double inv2a = 1.0 / two_a;
+    if (!(two_a >= 0x1p-100 && two_a <= 0x1p100)) return 2;
+    const double inv2a = rcp_refined(two_a);  // within 1 ulp of 1/2a: far inside the Δ margin
     bool blocked = false, undecided = false;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
@@ -530,10 +581,11 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
                                          const Hit& h, d3 lpos, d3 E, d3 lcenter, double lrad,
                                          double bias, int nchunks, d3& diff, d3& spec,
                                          Counts& cnt, const Masks<MAXC>* pre = nullptr) {
-    const d3 v = lpos - P;
-    const double dist = length(v);
+    double dist = 0.0, inv_d2 = 0.0;
+    d3 L = mk(0.0, 0.0, 0.0);
+    if (active) light_dir(lpos - P, dist, L, inv_d2);  // skipped by waves with no hit lane
     const bool reach = active && !(dist <= 0.0);
-    const d3 L = reach ? sdiv(v, dist) : mk(0.0, 0.0, 0.0);
+    if (!reach) L = mk(0.0, 0.0, 0.0);
     const double ndl = smax(0.0, dot(n, L));
     const bool need = reach && !(ndl <= 0.0) && !(dist <= bias);
     const d3 so = P + n * bias;
@@ -546,7 +598,6 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     double T = occ == 1 ? 0.0 : 1.0;
     if (occ == 2) T = pk_transmittance<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
     if (T <= bias) return;
-    const double inv_d2 = 1.0 / (dist * dist);
     diff = diff + ((E * inv_d2) * ndl) * T;
     if constexpr ((FEAT & kFeatSpec) != 0) {
         const double* m = pk_material(S, h);
@@ -666,10 +717,24 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
             // shading inputs (Scene.h:147-154); misses carry harmless placeholders
             const d3 hp = cam + d * h.t;
             const d3 gn = hit ? pk_normal(S, h, hp) : mk(0.0, 1.0, 0.0);
-            const d3 inc = unit(d);
-            const bool front = dot(gn, inc) < 0.0;
+            // frontFace = n·normalize(d) < 0 (Scene.h:148-150).  d is a unit vector (or zero),
+            // so normalize(d) = d/l·(1+δ) with l = 1 ± 4ε and |δ| ≤ ε; both dot products are
+            // within 5ε·S of their exact values, S = Σ|n_i·d_i| — when |n·d| > 1e-14·S they have
+            // the same sign, and the second normalize (3 divisions) is only needed otherwise.
+            // `view` is only read by the Blinn-Phong term.
+            bool front;
+            d3 view = mk(0.0, 0.0, 0.0);
+            if constexpr ((FEAT & kFeatSpec) != 0) {
+                const d3 inc = unit(d);
+                front = dot(gn, inc) < 0.0;
+                view = -inc;
+            } else {
+                const double nd = dot(gn, d);
+                const double sabs = fabs(gn.x * d.x) + fabs(gn.y * d.y) + fabs(gn.z * d.z);
+                if (fabs(nd) > 1e-14 * sabs && sabs > 1e-200) front = nd < 0.0;
+                else front = dot(gn, unit(d)) < 0.0;
+            }
             const d3 n0 = front ? gn : -gn;
-            const d3 view = -inc;
             const d3 n = unit(n0);  // directLightning's own normalize (Scene.h:81)
             d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
             for (int l = 0; l < nl; ++l) {

@@ -267,4 +267,33 @@ hipError_t launch_debug_f64(const double* x, const double* y, size_t n, double* 
     return hipGetLastError();
 }
 
+// Test hook for the sqrt/division cores (rt_device.hpp): per input vector v, the fast and the
+// compiler-lowered exact results side by side (a test compares them bit for bit).
+//   out[16i + 0..2]  unit(v)          out[16i + 3..5]   unit_exact(v)
+//   out[16i + 6..10] light_dir(v): dist, L, 1/(dist·dist)
+//   out[16i + 11..15] exact: sqrt(v·v), v/dist, 1/(dist·dist)
+__global__ void debug_vec_kernel(const double* v, size_t n, double* out) {
+    const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const d3 a = mk(v[3 * i], v[3 * i + 1], v[3 * i + 2]);
+    double* o = out + 16 * i;
+    const d3 u = unit(a), ue = unit_exact(a);
+    double dist, inv_d2;
+    d3 L;
+    light_dir(a, dist, L, inv_d2);
+    const double de = length(a);
+    const d3 Le = sdiv(a, de);
+    const double ie = 1.0 / (de * de);
+    const double vals[16] = {u.x,  u.y,  u.z,  ue.x, ue.y, ue.z, dist, L.x,
+                             L.y,  L.z,  inv_d2, de, Le.x, Le.y, Le.z, ie};
+    for (int k = 0; k < 16; ++k) o[k] = vals[k];
+}
+
+hipError_t launch_debug_vec(const double* v, size_t n, double* out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const unsigned blocks = static_cast<unsigned>((n + 255) / 256);
+    hipLaunchKernelGGL(debug_vec_kernel, dim3(blocks), dim3(256), 0, stream, v, n, out);
+    return hipGetLastError();
+}
+
 }  // namespace rtamd

@@ -348,8 +348,8 @@ __device__ __forceinline__ int occlusion_opaque(const SceneView& S, d3 o, d3 d, 
     if (S.nt > 0) return -1;
     const double a = dot(d, d);
     const double two_a = 2.0 * a, four_a = 4.0 * a;
-    if (!(two_a > 0.0)) return -1;
-    const double inv2a = 1.0 / two_a;
+    if (!(two_a >= 0x1p-100 && two_a <= 0x1p100)) return -1;
+    const double inv2a = rcp_refined(two_a);  // within 1 ulp of 1/2a: far inside the Δ margin
     bool blocked = false, undecided = false;
     for (int i = 0; i < S.ns; ++i) {
         const double* s = S.sph + kSphStride * i;
@@ -411,10 +411,10 @@ template <bool COUNT, bool OPQ>
 __device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 view, const Mat& m,
                                            d3 lpos, d3 E, double bias, d3& diff, d3& spec,
                                            Counts& cnt) {
-    const d3 v = lpos - P;
-    const double dist = length(v);
+    double dist, inv_d2;
+    d3 L;
+    light_dir(lpos - P, dist, L, inv_d2);
     if (dist <= 0.0) return;
-    const d3 L = sdiv(v, dist);
     const double ndl = smax(0.0, dot(n, L));
     if (ndl <= 0.0) return;
     if (dist <= bias) return;
@@ -427,7 +427,6 @@ __device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 vi
         T = transmittance(S, P + n * bias, L, dist - bias, bias);
     }
     if (T <= bias) return;
-    const double inv_d2 = 1.0 / (dist * dist);
     diff = diff + ((E * inv_d2) * ndl) * T;
     if (m.transparency <= 0.0 && m.specular > 0.0) {
         const d3 H = unit(L + view);

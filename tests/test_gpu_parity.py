@@ -95,6 +95,52 @@ def test_device_div_sqrt_edge_cases(ctx):
         assert _same_bits(out[:, 1], np.sqrt(x))
 
 
+def _vec_inputs():
+    rng = np.random.default_rng(23)
+    n = 40000
+    mag = lambda k: np.exp2(rng.uniform(-1074, 1023, k)) * rng.choice([-1.0, 1.0], k)
+    vs = [mag(3 * n).reshape(-1, 3),                                   # every binary64 range
+          rng.uniform(-50, 50, (n, 3)),                                # scene-scale vectors
+          rng.uniform(-1, 1, (n, 3)) * np.exp2(rng.uniform(-45, 65, (n, 1))),  # around the gates
+          rng.normal(size=(n, 3))]
+    u = rng.normal(size=(n, 3))
+    vs.append(u / np.sqrt((u * u).sum(1, keepdims=True)))             # unit: the 2nd normalize
+    # components at the numerator gate (2^-900) and zero / negative zero components
+    g = rng.uniform(-1, 1, (n, 3))
+    g[:, 0] = np.exp2(rng.uniform(-905, -895, n)) * rng.choice([-1.0, 1.0], n)
+    g[: n // 4, 1] = 0.0
+    g[n // 4: n // 2, 2] = -0.0
+    vs.append(g)
+    # length^2 exactly at the gates 2^-78 and 2^120, and axis-aligned unit vectors
+    vs.append(np.array([[2.0 ** -39, 0.0, 0.0], [2.0 ** 60, 0.0, 0.0],
+                        [2.0 ** -39.5, 2.0 ** -39.5, 1e-300], [1.0, 0.0, 0.0], [0.0, -1.0, 0.0],
+                        [0.6, 0.8, 0.0], [3.0, 4.0, 12.0], [0.0, 0.0, 0.0],
+                        [np.inf, 1.0, 1.0], [np.nan, 1.0, 1.0], [1e-12, 0.0, 0.0],
+                        [1e-12 * (1 + 2 ** -52), 0.0, 0.0], [5e-324, 0.0, 0.0]]))
+    return np.concatenate(vs)
+
+
+def test_fast_exact_cores(ctx):
+    """The sqrt / division cores (rt_device.hpp: unit(), light_dir()) return the same bits as the
+    compiler's correctly rounded lowering for every input (the cores run only inside their
+    ranges, the exact lowering outside), and both equal numpy's IEEE results."""
+    v = _vec_inputs()
+    with np.errstate(all="ignore"):
+        out = ctx.debug_vec_ops(v)
+        assert _same_bits(out[:, 0:3], out[:, 3:6])        # unit == unit_exact
+        ok = out[:, 6] > 0                                  # light_dir vs exact where dist > 0
+        assert _same_bits(out[:, 6], out[:, 11])
+        assert _same_bits(out[ok, 7:11], out[ok, 12:16])
+        # numpy: Vec3::length / normalize (Math.h:27-37)
+        dist = np.sqrt((v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1]) + v[:, 2] * v[:, 2])
+        assert _same_bits(out[:, 6], dist)
+        assert _same_bits(out[ok, 7:10], v[ok] / dist[ok, None])
+        assert _same_bits(out[ok, 10], 1.0 / (dist[ok] * dist[ok]))
+        ref = np.where((dist <= 1e-12)[:, None], 0.0,
+                       np.where((dist == 1.0)[:, None], v, v / dist[:, None]))
+        assert _same_bits(out[:, 0:3], ref)
+
+
 @pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4", "mirror", "glass", "mesh"])
 def test_small_scenes_vs_reference_golden(ctx, golden, name):
     sc = make_config(name, *SMALL)

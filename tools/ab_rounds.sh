@@ -1,0 +1,9 @@
+#!/bin/bash
+# Dev tool: interleaved A/B rounds (in-tree lib + tools/variants/*.so), N rounds of ab_time.
+set -e
+N=${N:-3}
+for r in $(seq $N); do
+  for lib in raytracingengine_amd/librtamd.so tools/variants/*.so; do
+    echo "== $(basename $lib) $(RTAMD_LIB=$lib timeout -k 10 120 python tools/ab_time.py "$@" | tr '\n' ' ')"
+  done
+done

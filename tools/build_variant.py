@@ -1,0 +1,42 @@
+"""Dev tool: build an A/B (or ablation) library from a patched copy of one source.
+
+    python tools/build_variant.py NAME FILE 'old text' 'new text' ['old' 'new' ...] [-D MACRO ...]
+
+FILE is a source under raytracingengine_amd/csrc; the copy (with every replacement applied,
+each must match) is compiled with the in-tree flags and linked with the in-tree objects of the
+other sources into tools/variants/NAME.so (git-ignored).  Ablation builds render wrong images;
+time them with tools/ab_time.py / tools/pmc_ab.sh only.
+"""
+import os, shutil, subprocess, sys, tempfile
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from raytracingengine_amd import build as B
+
+args = sys.argv[1:]
+defs = []
+while "-D" in args:
+    i = args.index("-D")
+    defs.append("-D" + args[i + 1])
+    del args[i:i + 2]
+name, fname, reps = args[0], args[1], args[2:]
+assert len(reps) % 2 == 0
+B.build_library()
+tmp = tempfile.mkdtemp()
+src_dir = os.path.join(tmp, "csrc")
+shutil.copytree(B.CSRC, src_dir)
+path = os.path.join(src_dir, fname)
+text = open(path).read()
+for old, new in zip(reps[::2], reps[1::2]):
+    assert old in text, f"patch text not found: {old[:60]!r}"
+    text = text.replace(old, new)
+open(path, "w").write(text)
+obj = os.path.join(tmp, fname + ".o")
+inc = f"-I{os.path.join(B.ROOT, 'include')}"
+subprocess.check_call([B.HIPCC, *B.HIP_FLAGS, *B.EXTRA_FLAGS.get(fname, []), *defs, inc, "-c",
+                       "-o", obj, path], stderr=subprocess.DEVNULL)
+objs = [obj if s == fname else os.path.join(B.OBJ_DIR, s + ".o") for s in B.SOURCES]
+out_dir = os.path.join(B.ROOT, "tools", "variants")
+os.makedirs(out_dir, exist_ok=True)
+out = os.path.join(out_dir, name + ".so")
+subprocess.check_call([B.HIPCC, *B.HIP_FLAGS, "-shared", "-o", out, *objs])
+shutil.rmtree(tmp)
+print(out)
