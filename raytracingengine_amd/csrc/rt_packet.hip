@@ -95,6 +95,7 @@ struct PacketScene {
     const double* sph;   // LDS: cx cy cz r²
     const double* rad;   // LDS: radius (culling only)
     const double* pre;   // LDS: camera-ray oc.xyz, oc·oc − r²
+    const float* cone;   // LDS: camera-cone terms (cone_terms)
     const double* pl;    // LDS: planes (px py pz nx ny nz (p−cam)·n −)
     const double* lt;    // LDS: point lights
     const double* tri;   // HBM
@@ -142,9 +143,29 @@ __device__ __forceinline__ float dot3f(float ax, float ay, float az, float bx, f
 // Error bound (d = |C−o|): |C−o|² and the dot product carry < 5e-7·d² and 3e-7·d; spheres with
 // d ≤ 1.01·r' are kept outright, so |C−o|²−r'² ≥ 0.0199·r'² and its square root is off by at
 // most 2.5e-6·d; total < 3e-6·d against a slack of 2e-5·d.
+// The cone test's per-sphere terms depend on the camera only (every camera ray starts there),
+// so each workgroup forms them once into LDS (8 floats per sphere: vx vy vz q | rr dv slack r),
+// with q = NaN for spheres that are always kept; the same FP32 expressions, so the same masks.
+__device__ __forceinline__ void cone_terms(const double* s, double radius, d3 o, float* out) {
+    const float r = f32_up(radius);
+    const float vx = static_cast<float>(s[0] - o.x), vy = static_cast<float>(s[1] - o.y),
+                vz = static_cast<float>(s[2] - o.z);
+    const float dv2 = dot3f(vx, vy, vz, vx, vy, vz);
+    const float rr = r * (1.0f + static_cast<float>(kCullRel));
+    const float dv = sqrtf(dv2);
+    const bool always = !(dv > 1.01f * rr) || !(dv <= static_cast<float>(kFarRatio) * r);
+    out[0] = vx;
+    out[1] = vy;
+    out[2] = vz;
+    out[3] = always ? __builtin_nanf("") : sqrtf(dv2 - rr * rr);  // |C−o|·cos β
+    out[4] = rr;
+    out[5] = dv;
+    out[6] = kF32Slack * dv;
+    out[7] = r;  // the capsule test's radius
+}
+
 template <int MAXC>
-__device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 o, d3 axis,
-                                                 double cos_min) {
+__device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 axis, double cos_min) {
     Masks<MAXC> M;
     const int lane = threadIdx.x & 63;
     const float cs = static_cast<float>(cos_min) * (1.0f - 1e-6f);  // rounded down (cs > 0)
@@ -156,21 +177,12 @@ __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 o, d3 
         const int k = c * 64 + lane;
         bool keep = false;
         if (k < S.ns) {
-            const double* s = S.sph + kSphStride * k;
-            const float r = f32_up(S.rad[k]);
-            const float vx = static_cast<float>(s[0] - o.x), vy = static_cast<float>(s[1] - o.y),
-                        vz = static_cast<float>(s[2] - o.z);
-            const float dv2 = dot3f(vx, vy, vz, vx, vy, vz);
-            const float rr = r * (1.0f + static_cast<float>(kCullRel));
-            const float dv = sqrtf(dv2);
-            if (!(dv > 1.01f * rr) || !(dv <= static_cast<float>(kFarRatio) * r)) {
-                keep = true;
-            } else {
-                const float q = sqrtf(dv2 - rr * rr);  // |C−o|·cos β
-                const float slack = kF32Slack * dv;
-                if (!(q > -cs * dv + slack)) keep = true;  // θ + β ≥ π
-                else keep = !(dot3f(vx, vy, vz, ax, ay, az) < cs * q - sn * rr - slack);
-            }
+            const float4 a = reinterpret_cast<const float4*>(S.cone)[2 * k];
+            const float4 b = reinterpret_cast<const float4*>(S.cone)[2 * k + 1];
+            const float q = a.w, rr = b.x, dv = b.y, slack = b.z;
+            // θ + β ≥ π, or the axis is outside the cone around C−o (NaN q: always kept)
+            keep = !(q > -cs * dv + slack) ||
+                   !(dot3f(a.x, a.y, a.z, ax, ay, az) < cs * q - sn * rr - slack);
         }
         M.m[c] = __ballot(keep);
     }
@@ -614,11 +626,12 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
 
 template <int MAXC, int FEAT, bool COUNT>
 __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LEAN_WAVES : 1) void packet_direct_kernel(TraceParams P) {
-    extern __shared__ double smem[];
+    extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
     const int ns = P.ns, np = P.np, nl = P.nl;
-    double* s_sph = smem;
-    double* s_rad = s_sph + kSphStride * ns;
+    double* s_sph = smem;                                         // 32·ns bytes
+    float* s_cone = reinterpret_cast<float*>(s_sph + kSphStride * ns);  // 16-byte aligned
+    double* s_rad = s_sph + (kSphStride + 4) * ns;
     double* s_pre = s_rad + ns;
     double* s_pl = s_pre + 4 * ns;
     double* s_lt = s_pl + kPlStride * np;
@@ -627,6 +640,7 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
     for (int i = tid; i < ns; i += kWgThreads) {
         const double* s = P.sph + kSphStride * i;
         s_rad[i] = sqrt(s[3]);  // culling radius (only ever used with a margin)
+        cone_terms(s, s_rad[i], cam, s_cone + 8 * i);
         // camera-ray constants of Sphere::Intersect (Shape.h:73,77)
         const d3 oc = cam - mk(s[0], s[1], s[2]);
         s_pre[4 * i + 0] = oc.x;
@@ -648,6 +662,7 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
     PacketScene S;
     S.sph = s_sph;
     S.rad = s_rad;
+    S.cone = s_cone;
     S.pre = s_pre;
     S.pl = s_pl;
     S.lt = s_lt;
@@ -707,7 +722,7 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
             const double cos_min =
                 static_cast<double>(wave_red<0>(__double2float_rd(dot(d, axis)))) - 1e-7;
             const bool ok = isfinite(cos_min) && cos_min > 0.0;  // cones narrower than 90°
-            const Masks<MAXC> M = ok ? cull_cone<MAXC>(S, cam, axis, cos_min)
+            const Masks<MAXC> M = ok ? cull_cone<MAXC>(S, axis, cos_min)
                                      : all_candidates<MAXC>(ns);
             Hit h;
             h.t = 0.0;
@@ -818,7 +833,7 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
 }
 
 size_t packet_lds_bytes(int ns, int np, int nl) {
-    return sizeof(double) * (static_cast<size_t>(kSphStride + 1 + 4) * ns +
+    return sizeof(double) * (static_cast<size_t>(kSphStride + 1 + 4 + 4) * ns +
                              static_cast<size_t>(kPlStride) * np + static_cast<size_t>(kLtStride) * nl);
 }
 
