@@ -136,6 +136,9 @@ __device__ __forceinline__ float f32_up(double v) { return static_cast<float>(v)
 __device__ __forceinline__ float dot3f(float ax, float ay, float az, float bx, float by, float bz) {
     return ax * bx + ay * by + az * bz;
 }
+// v_sqrt_f32 without the compiler's correct-rounding fix-up (≤ 1 ulp, 1.2e-7 relative): every
+// FP32 square root of the culls and classifications carries a margin of ≥ 5e-7 for it.
+__device__ __forceinline__ float sqrt_f32(float x) { return __builtin_amdgcn_sqrtf(x); }
 
 // Camera-ray packet: origin `o` shared, directions within the cone (axis, cos_min), cos_min > 0.
 // Sphere (C, r) is kept iff angle(C−o, axis) ≤ θ + β, sin β = r'/|C−o| (r' = inflated r),
@@ -152,12 +155,12 @@ __device__ __forceinline__ void cone_terms(const double* s, double radius, d3 o,
                 vz = static_cast<float>(s[2] - o.z);
     const float dv2 = dot3f(vx, vy, vz, vx, vy, vz);
     const float rr = r * (1.0f + static_cast<float>(kCullRel));
-    const float dv = sqrtf(dv2);
+    const float dv = sqrt_f32(dv2);
     const bool always = !(dv > 1.01f * rr) || !(dv <= static_cast<float>(kFarRatio) * r);
     out[0] = vx;
     out[1] = vy;
     out[2] = vz;
-    out[3] = always ? __builtin_nanf("") : sqrtf(dv2 - rr * rr);  // |C−o|·cos β
+    out[3] = always ? __builtin_nanf("") : sqrt_f32(dv2 - rr * rr);  // |C−o|·cos β
     out[4] = rr;
     out[5] = dv;
     out[6] = kF32Slack * dv;
@@ -169,7 +172,7 @@ __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 axis, 
     Masks<MAXC> M;
     const int lane = threadIdx.x & 63;
     const float cs = static_cast<float>(cos_min) * (1.0f - 1e-6f);  // rounded down (cs > 0)
-    const float sn = sqrtf(fmaxf(0.0f, 1.0f - cs * cs)) * (1.0f + 1e-5f);  // rounded up
+    const float sn = sqrt_f32(fmaxf(0.0f, 1.0f - cs * cs)) * (1.0f + 1e-5f);  // rounded up
     const float ax = static_cast<float>(axis.x), ay = static_cast<float>(axis.y),
                 az = static_cast<float>(axis.z);
 #pragma unroll
@@ -202,6 +205,7 @@ __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, 
     const float sx = static_cast<float>(L.x - c.x), sy = static_cast<float>(L.y - c.y),
                 sz = static_cast<float>(L.z - c.z);
     const float sl2 = dot3f(sx, sy, sz, sx, sy, sz);
+    const float inv_sl2 = 1.0f / sl2;  // wave-uniform; only read when sl2 > 0
     const float Rc = fmaxf(R, f32_up(RL));
 #pragma unroll
     for (int ch = 0; ch < MAXC; ++ch) {
@@ -221,7 +225,7 @@ __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, 
                 const float wx = vx - sx, wy = vy - sy, wz = vz - sz;
                 d2 = dot3f(wx, wy, wz, wx, wy, wz);
             } else {
-                d2 = vv - (vs * vs) / sl2;
+                d2 = vv - (vs * vs) * inv_sl2;  // one more rounding than a division: ≪ slack
             }
             const float lim = (r + Rc) * (1.0f + static_cast<float>(kCullRel));
             const float far = static_cast<float>(kFarRatio) * r - Rc;
@@ -524,9 +528,9 @@ __device__ __forceinline__ int pk_occlusion(const PacketScene& S, const Masks<MA
                 undecided = true;
                 continue;
             }
-            // |sq − fl(√disc)| ≤ 5e-7·√disc (FP32 conversion + sqrtf), so both roots are within
+            // |sq − fl(√disc)| ≤ 5e-7·√disc (FP32 conversion + sqrt_f32), so both roots are within
             // Δ = 2e-6·(|b| + sq)/2a of the reference's fl(fl(−b ∓ sq)/2a) (2× margin)
-            const double sq = static_cast<double>(sqrtf(static_cast<float>(disc)));
+            const double sq = static_cast<double>(sqrt_f32(static_cast<float>(disc)));
             const double delta = 2e-6 * (fabs(b) + sq) * inv2a;
             double t = (-b - sq) * inv2a;
             if (!(t >= 1e-6 + delta)) {
@@ -579,7 +583,7 @@ __device__ __forceinline__ Masks<MAXC> shadow_masks(const PacketScene& S, bool c
     if (casting_lane) {  // |so − c| in FP32, rounded up (FP64 differences, 5e-7 rel. error)
         const float dx = static_cast<float>(so.x - c.x), dy = static_cast<float>(so.y - c.y),
                     dz = static_cast<float>(so.z - c.z);
-        r_lane = sqrtf(dot3f(dx, dy, dz, dx, dy, dz)) * (1.0f + 1e-5f);
+        r_lane = sqrt_f32(dot3f(dx, dy, dz, dx, dy, dz)) * (1.0f + 1e-5f);
     }
     const float R = wave_red<1>(r_lane);
     return __ballot(bad) || !isfinite(R) ? all_candidates<MAXC>(S.ns)

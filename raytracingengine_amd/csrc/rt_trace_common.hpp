@@ -363,7 +363,7 @@ __device__ __forceinline__ int occlusion_opaque(const SceneView& S, d3 o, d3 d, 
             continue;
         }
         // |sq − fl(√disc)| ≤ 5e-7·√disc, so both roots are within Δ of the reference's
-        const double sq = static_cast<double>(sqrtf(static_cast<float>(disc)));
+        const double sq = static_cast<double>(__builtin_amdgcn_sqrtf(static_cast<float>(disc)));  // ≤ 1 ulp
         const double delta = 2e-6 * (fabs(b) + sq) * inv2a;
         double t = (-b - sq) * inv2a;
         if (!(t >= 1e-6 + delta)) {
