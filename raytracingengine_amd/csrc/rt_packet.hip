@@ -61,24 +61,30 @@ constexpr int kFeatAll = 15;
 #endif
 
 // ------------------------------------------------------------------ wave reductions (FP32)
-// Every lane must be active.  Four DPP steps reduce each 16-lane row (quad xor-1, quad xor-2,
-// half-mirror, mirror: every lane of a row ends with the row's result), then the four row
-// values are read into SGPRs and combined in the same order in every lane.
+// Every lane must be active.  Floats are reduced as order-preserving int32 keys (sign-magnitude
+// to two's complement), so each step is one integer min/max on a DPP-permuted operand: four
+// steps reduce each 16-lane row (quad xor-1, quad xor-2, half-mirror, mirror), then the four row
+// values are combined in SGPRs.  NaN keys sort above +inf (a max returns NaN, a min skips it).
 template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+__device__ __forceinline__ int dpp(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
 }
-__device__ __forceinline__ float lane_f(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+__device__ __forceinline__ int f2key(float v) {
+    const int b = __float_as_int(v);
+    return b ^ ((b >> 31) & 0x7fffffff);
 }
+__device__ __forceinline__ float key2f(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
 template <int OP>  // 0 min, 1 max
-__device__ __forceinline__ float wave_red(float v) {
-    auto op = [](float a, float b) { return OP == 0 ? fminf(a, b) : fmaxf(a, b); };
+__device__ __forceinline__ float wave_red(float x) {
+    auto op = [](int a, int b) { return OP == 0 ? (a < b ? a : b) : (a < b ? b : a); };
+    int v = f2key(x);
     v = op(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
     v = op(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
     v = op(v, dpp<0x141>(v));  // row_half_mirror
     v = op(v, dpp<0x140>(v));  // row_mirror
-    return op(op(lane_f(v, 0), lane_f(v, 16)), op(lane_f(v, 32), lane_f(v, 48)));
+    const int r = op(op(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+                     op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+    return key2f(r);
 }
 
 // Lane `l`'s double / vector, broadcast to every lane (exact: a bit copy via SGPRs).
@@ -721,10 +727,11 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
         } else {
             if (COUNT && valid) cnt.trace++;
             // camera cone: axis = the tile's centre-lane direction (exact copy), half-angle
-            // from the wave minimum of the per-lane cosines, rounded down to FP32
+            // from the wave minimum of the per-lane cosines in FP32 (|cos| ≤ 1 + 2ε, so the
+            // conversion is off by ≤ 6e-8, inside the 1e-7 taken off)
             const d3 axis = lane_d3(d, (kPkH / 2) * kPkW + kPkW / 2);
             const double cos_min =
-                static_cast<double>(wave_red<0>(__double2float_rd(dot(d, axis)))) - 1e-7;
+                static_cast<double>(wave_red<0>(static_cast<float>(dot(d, axis)))) - 1e-7;
             const bool ok = isfinite(cos_min) && cos_min > 0.0;  // cones narrower than 90°
             const Masks<MAXC> M = ok ? cull_cone<MAXC>(S, axis, cos_min)
                                      : all_candidates<MAXC>(ns);
