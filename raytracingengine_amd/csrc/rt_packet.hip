@@ -59,6 +59,10 @@ constexpr int kFeatAll = 15;
 #ifndef RT_PACKET_LEAN_WAVES
 #define RT_PACKET_LEAN_WAVES 4
 #endif
+// ... and the lean single-sample variants (5 = at most 96 VGPRs)
+#ifndef RT_PACKET_AA1_WAVES
+#define RT_PACKET_AA1_WAVES 5
+#endif
 
 // ------------------------------------------------------------------ wave reductions (FP32)
 // Every lane must be active.  Floats are reduced as order-preserving int32 keys (sign-magnitude
@@ -634,8 +638,8 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     }
 }
 
-template <int MAXC, int FEAT, bool COUNT>
-__global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LEAN_WAVES : 1) void packet_direct_kernel(TraceParams P) {
+template <int MAXC, int FEAT, bool COUNT, bool MULTI>  // MULTI = false: exactly one sample (AA = 1)
+__global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? (MULTI ? RT_PACKET_LEAN_WAVES : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
     const int ns = P.ns, np = P.np, nl = P.nl;
@@ -708,7 +712,8 @@ __global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? RT_PACKET_LE
 
     d3 acc = mk(0.0, 0.0, 0.0);
     int samples = 0;
-    for (int s = 0; s < P.aa; ++s) {
+    const int nsamples = MULTI ? P.aa : 1;
+    for (int s = 0; s < nsamples; ++s) {
         // Camera::getRay (Math.h:99-121)
         double sx = static_cast<double>(xc) - static_cast<double>(P.width) / 2.0;
         double sy = static_cast<double>(P.height) / 2.0 - static_cast<double>(y);
@@ -855,8 +860,12 @@ static void launch_packet_variant(const TraceParams& p, bool count, size_t lds, 
     const dim3 block(kWgThreads);
     const dim3 grid((p.width + kPkW * kWgWavesX - 1) / (kPkW * kWgWavesX),
                     (p.rows + kPkH * kWgWavesY - 1) / (kPkH * kWgWavesY));
-    if (count) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, true>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false>), grid, block, lds, stream, p);
+    // the single-sample variant keeps no accumulator live across the trace (AA = 1, the
+    // reference default for a preview and the bench's configuration); counting passes use the
+    // general one
+    if (count) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, true, true>), grid, block, lds, stream, p);
+    else if (p.aa == 1) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, false>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, true>), grid, block, lds, stream, p);
 }
 
 template <int MAXC>
