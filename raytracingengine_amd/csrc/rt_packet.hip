@@ -59,7 +59,7 @@ constexpr int kFeatAll = 15;
 #ifndef RT_PACKET_LEAN_WAVES
 #define RT_PACKET_LEAN_WAVES 4
 #endif
-// ... and the lean single-sample variants (5 = at most 96 VGPRs)
+// ... and the single-sample variants without Blinn-Phong / triangles (5 = at most 96 VGPRs)
 #ifndef RT_PACKET_AA1_WAVES
 #define RT_PACKET_AA1_WAVES 5
 #endif
@@ -639,7 +639,7 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
 }
 
 template <int MAXC, int FEAT, bool COUNT, bool MULTI>  // MULTI = false: exactly one sample (AA = 1)
-__global__ __launch_bounds__(kWgThreads, (FEAT == 0 && MAXC <= 4) ? (MULTI ? RT_PACKET_LEAN_WAVES : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
+__global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
     const int ns = P.ns, np = P.np, nl = P.nl;
