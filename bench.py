@@ -100,15 +100,21 @@ def cpu_baseline(sc, rays_per_frame: int, frames: int):
         ms1 = [(time.perf_counter() - t0) * 1e3]
     single = {"value": rays_per_frame / (ms1[0] / 1e3) / 1e6, "cores": 1,
               "ms_per_frame": ms1[0]}
+    multi = {"value": rays_per_frame / (med / 1e3) / 1e6, "cores": used, "ms_per_frame": med}
+    # The box's granted CPU share can be smaller than the thread count OpenMP is given (its
+    # frames then run slower than one thread's); the baseline is the faster of the two runs.
+    best = multi if multi["value"] >= single["value"] else single
     return {
-        "value": rays_per_frame / (med / 1e3) / 1e6,
+        "value": best["value"],
         "unit": "Mrays/s",
-        "cores": used,
+        "cores": best["cores"],
         "kind": kind,
         "sample": f"{len(ms)} full {sc.camera.width}x{sc.camera.height} frames of config "
-                  f"{sc.name} (Scene::RenderImage only, first frame warm-up; median "
-                  f"{med:.1f} ms/frame)",
-        "ms_per_frame": med,
+                  f"{sc.name} on {used} threads (Scene::RenderImage only, first frame warm-up; "
+                  f"median {med:.1f} ms/frame) and one frame on 1 thread "
+                  f"({ms1[0]:.1f} ms); value = the faster",
+        "ms_per_frame": best["ms_per_frame"],
+        "all_threads": multi,
         "single_core": single,
     }
 

@@ -3,7 +3,7 @@
 set -e
 N=${N:-3}
 for r in $(seq $N); do
-  for lib in raytracingengine_amd/librtamd.so tools/variants/*.so; do
+  for lib in raytracingengine_amd/librtamd.so $(ls tools/variants/*.so 2>/dev/null); do
     echo "== $(basename $lib) $(RTAMD_LIB=$lib timeout -k 10 120 python tools/ab_time.py "$@" | tr '\n' ' ')"
   done
 done

@@ -4,7 +4,7 @@
 # (AB_TOOL=tools/ab_time.py times the headline mode: f64 HDR + fused Reinhard bytes)
 set -e
 mkdir -p gpurun_out
-for lib in raytracingengine_amd/librtamd.so tools/variants/*.so; do
+for lib in raytracingengine_amd/librtamd.so $(ls tools/variants/*.so 2>/dev/null); do
   echo "== $lib"
   RTAMD_LIB=$lib timeout -k 10 300 python ${AB_TOOL:-tools/ab_kernels.py} "$@"
 done

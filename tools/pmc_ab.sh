@@ -5,7 +5,7 @@ set -e
 export TMPDIR=/tmp
 OUT=gpurun_out/pmcab
 mkdir -p $OUT
-for lib in raytracingengine_amd/librtamd.so tools/variants/*.so; do
+for lib in raytracingengine_amd/librtamd.so $(ls tools/variants/*.so 2>/dev/null); do
   tag=$(basename $lib .so)
   for cfg in "$@"; do
     RTAMD_LIB=$lib timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_INSTS_VALU_TRANS_F64 SQ_ACTIVE_INST_VALU \
