@@ -115,6 +115,13 @@ struct PacketScene {
     int ns, np, nt, nl;
 };
 
+// Closest hit of the packet kernel: t and the primitive's index in the material table order
+// [spheres | planes | triangles] (one register instead of a kind and a per-kind index).
+struct PkHit {
+    double t;
+    int prim;
+};
+
 // Candidate masks: MAXC chunks of 64 spheres.  m[c] is wave-uniform (a ballot result).
 template <int MAXC>
 struct Masks {
@@ -251,7 +258,7 @@ __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, 
 // Requires two_a > 0 (then t0 ≤ t1 exactly); divisions are skipped when the candidate
 // provably cannot be strictly closer than `best`.
 __device__ __forceinline__ void sphere_roots(double b, double disc, double two_a, int i,
-                                             bool& found, double& best, int& kind, int& idx) {
+                                             bool& found, double& best, int& prim) {
     if (disc < 0.0) return;
     const double sq = sqrt(disc);
     const double n0 = -b - sq;
@@ -264,8 +271,7 @@ __device__ __forceinline__ void sphere_roots(double b, double disc, double two_a
     if (!found || t < best) {
         found = true;
         best = t;
-        kind = 1;
-        idx = i;
+        prim = i;
     }
 }
 
@@ -275,8 +281,7 @@ __device__ __forceinline__ void sphere_roots(double b, double disc, double two_a
 // and through the core, so the 1e-6 test (the only use of such a root) decides alike.  Other
 // discriminants take the literal path.  t0 ≤ t1 as in sphere_roots.
 __device__ __forceinline__ void sphere_roots_core(double b, double disc, double two_a, double r2a,
-                                                  int i, bool& found, double& best, int& kind,
-                                                  int& idx) {
+                                                  int i, bool& found, double& best, int& prim) {
     if (disc < 0.0) return;
     double t;
     if (disc >= 0x1p-767 && disc <= 0x1.fffffffffffffp+1023) {
@@ -297,15 +302,13 @@ __device__ __forceinline__ void sphere_roots_core(double b, double disc, double 
     if (!found || t < best) {
         found = true;
         best = t;
-        kind = 1;
-        idx = i;
+        prim = i;
     }
 }
 
 // The reference's literal root selection, for degenerate directions (2a not > 0).
 __device__ __forceinline__ void sphere_roots_literal(double b, double disc, double two_a, int i,
-                                                     bool& found, double& best, int& kind,
-                                                     int& idx) {
+                                                     bool& found, double& best, int& prim) {
     if (disc < 0.0) return;
     const double sq = sqrt(disc);
     double t0 = (-b - sq) / two_a;
@@ -323,14 +326,13 @@ __device__ __forceinline__ void sphere_roots_literal(double b, double disc, doub
     if (!found || t < best) {
         found = true;
         best = t;
-        kind = 1;
-        idx = i;
+        prim = i;
     }
 }
 
 // Plane::Intersect (Shape.h:149-159) given num = (p − o)·n and denom = n·d.
-__device__ __forceinline__ void plane_t(double num, double denom, int i, bool& found,
-                                        double& best, int& kind, int& idx) {
+__device__ __forceinline__ void plane_t(double num, double denom, int p, bool& found,
+                                        double& best, int& prim) {
     if (!(fabs(denom) > 1e-6)) return;
     if (found) {  // skip the division when t = num/denom is provably >= best
         const double lim = (best * denom) * kNoWin;
@@ -340,17 +342,19 @@ __device__ __forceinline__ void plane_t(double num, double denom, int i, bool& f
     if (t >= 0.0 && (!found || t < best)) {
         found = true;
         best = t;
-        kind = 2;
-        idx = i;
+        prim = p;
     }
 }
 
 template <int FEAT>
 __device__ __forceinline__ void triangles(const PacketScene& S, d3 o, d3 d, bool& found,
-                                          double& best, int& kind, int& idx) {
+                                          double& best, int& prim) {
     if (!(FEAT & kFeatTris)) return;
+    const int base = S.ns + S.np;
     if (S.bvh) {
-        bvh_triangles(S.tri, S.bvh, S.bvh_tri, o, d, found, best, kind, idx);
+        int kind = 0, ti = -1;
+        bvh_triangles(S.tri, S.bvh, S.bvh_tri, o, d, found, best, kind, ti);
+        if (kind == 3) prim = base + ti;
         return;
     }
     for (int i = 0; i < S.nt; ++i) {
@@ -358,8 +362,7 @@ __device__ __forceinline__ void triangles(const PacketScene& S, d3 o, d3 d, bool
         if (tri_hit(S.tri, i, o, d, t) && (!found || t < best)) {
             found = true;
             best = t;
-            kind = 3;
-            idx = i;
+            prim = base + i;
         }
     }
 }
@@ -367,10 +370,10 @@ __device__ __forceinline__ void triangles(const PacketScene& S, d3 o, d3 d, bool
 // IntersectClosest for a camera ray (origin = the camera) over the candidate spheres.
 template <int MAXC, int FEAT>
 __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks<MAXC>& M,
-                                               int nchunks, d3 o, d3 d, Hit& h) {
+                                               int nchunks, d3 o, d3 d, PkHit& h) {
     bool found = false;
     double best = 0.0;
-    int kind = 0, idx = -1;
+    int prim = -1;
     const double a = dot(d, d);
     const double two_a = 2.0 * a, four_a = 4.0 * a;
     const bool regular = two_a > 0.0;
@@ -387,7 +390,7 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
                 const double* q = S.pre + 4 * i;
                 const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
                 const double disc = b * b - four_a * q[3];
-                sphere_roots_core(b, disc, two_a, r2a, i, found, best, kind, idx);
+                sphere_roots_core(b, disc, two_a, r2a, i, found, best, prim);
             }
         }
     } else {
@@ -401,29 +404,28 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
                 const double* q = S.pre + 4 * i;
                 const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
                 const double disc = b * b - four_a * q[3];
-                if (regular) sphere_roots(b, disc, two_a, i, found, best, kind, idx);
-                else sphere_roots_literal(b, disc, two_a, i, found, best, kind, idx);
+                if (regular) sphere_roots(b, disc, two_a, i, found, best, prim);
+                else sphere_roots_literal(b, disc, two_a, i, found, best, prim);
             }
         }
     }
     for (int i = 0; i < S.np; ++i) {
         const double* p = S.pl + kPlStride * i;
-        plane_t(p[6], dot(mk(p[3], p[4], p[5]), d), i, found, best, kind, idx);
+        plane_t(p[6], dot(mk(p[3], p[4], p[5]), d), S.ns + i, found, best, prim);
     }
-    triangles<FEAT>(S, o, d, found, best, kind, idx);
+    triangles<FEAT>(S, o, d, found, best, prim);
     h.t = best;
-    h.kind = kind;
-    h.idx = idx;
+    h.prim = prim;
     return found;
 }
 
 // IntersectClosest for an arbitrary ray over the candidate spheres.
 template <int MAXC, int FEAT>
 __device__ __forceinline__ bool closest_masked(const PacketScene& S, const Masks<MAXC>& M,
-                                               int nchunks, d3 o, d3 d, Hit& h) {
+                                               int nchunks, d3 o, d3 d, PkHit& h) {
     bool found = false;
     double best = 0.0;
-    int kind = 0, idx = -1;
+    int prim = -1;
     const double a = dot(d, d);
     const double two_a = 2.0 * a, four_a = 4.0 * a;
     const bool regular = two_a > 0.0;
@@ -439,37 +441,35 @@ __device__ __forceinline__ bool closest_masked(const PacketScene& S, const Masks
             const double b = 2.0 * dot(oc, d);
             const double cc = dot(oc, oc) - s[3];
             const double disc = b * b - four_a * cc;
-            if (regular) sphere_roots(b, disc, two_a, i, found, best, kind, idx);
-            else sphere_roots_literal(b, disc, two_a, i, found, best, kind, idx);
+            if (regular) sphere_roots(b, disc, two_a, i, found, best, prim);
+            else sphere_roots_literal(b, disc, two_a, i, found, best, prim);
         }
     }
     for (int i = 0; i < S.np; ++i) {
         const double* p = S.pl + kPlStride * i;
         const d3 n = mk(p[3], p[4], p[5]);
-        plane_t(dot(mk(p[0], p[1], p[2]) - o, n), dot(n, d), i, found, best, kind, idx);
+        plane_t(dot(mk(p[0], p[1], p[2]) - o, n), dot(n, d), S.ns + i, found, best, prim);
     }
-    triangles<FEAT>(S, o, d, found, best, kind, idx);
+    triangles<FEAT>(S, o, d, found, best, prim);
     h.t = best;
-    h.kind = kind;
-    h.idx = idx;
+    h.prim = prim;
     return found;
 }
 
-__device__ __forceinline__ const double* pk_material(const PacketScene& S, const Hit& h) {
-    const int base = h.kind == 1 ? 0 : (h.kind == 2 ? S.ns : S.ns + S.np);
-    return S.mat + kMatStride * (base + h.idx);
+__device__ __forceinline__ const double* pk_material(const PacketScene& S, const PkHit& h) {
+    return S.mat + kMatStride * h.prim;  // the table is [spheres | planes | triangles]
 }
 
-__device__ __forceinline__ d3 pk_normal(const PacketScene& S, const Hit& h, d3 p) {
-    if (h.kind == 1) {
-        const double* s = S.sph + kSphStride * h.idx;
+__device__ __forceinline__ d3 pk_normal(const PacketScene& S, const PkHit& h, d3 p) {
+    if (h.prim < S.ns) {
+        const double* s = S.sph + kSphStride * h.prim;
         return unit(p - mk(s[0], s[1], s[2]));
     }
-    if (h.kind == 2) {
-        const double* q = S.pl + kPlStride * h.idx;
+    if (h.prim < S.ns + S.np) {
+        const double* q = S.pl + kPlStride * (h.prim - S.ns);
         return mk(q[3], q[4], q[5]);
     }
-    const double* q = S.tri + kTriStride * h.idx;
+    const double* q = S.tri + kTriStride * (h.prim - S.ns - S.np);
     return mk(q[9], q[10], q[11]);
 }
 
@@ -481,7 +481,7 @@ __device__ __forceinline__ double pk_transmittance(const PacketScene& S, const M
     double T = 1.0, traveled = 0.0;
     int safety = 64;
     while (safety-- > 0 && T > 1e-4 && traveled < max_dist) {
-        Hit h;
+        PkHit h;
         if (!closest_masked<MAXC, FEAT>(S, M, nchunks, o, d, h)) break;
         const double t = h.t;
         if (t <= 0.0) {
@@ -604,7 +604,7 @@ __device__ __forceinline__ Masks<MAXC> shadow_masks(const PacketScene& S, bool c
 // (uniform control flow for the packet reductions); `active` lanes shade.
 template <int MAXC, int FEAT, bool COUNT>
 __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P, d3 n, d3 view,
-                                         const Hit& h, d3 lpos, d3 E, d3 lcenter, double lrad,
+                                         const PkHit& h, d3 lpos, d3 E, d3 lcenter, double lrad,
                                          double bias, int nchunks, d3& diff, d3& spec,
                                          Counts& cnt, const Masks<MAXC>* pre = nullptr) {
     double dist = 0.0, inv_d2 = 0.0;
@@ -740,10 +740,9 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
             const bool ok = isfinite(cos_min) && cos_min > 0.0;  // cones narrower than 90°
             const Masks<MAXC> M = ok ? cull_cone<MAXC>(S, axis, cos_min)
                                      : all_candidates<MAXC>(ns);
-            Hit h;
+            PkHit h;
             h.t = 0.0;
-            h.kind = 0;
-            h.idx = 0;
+            h.prim = 0;
             const bool hit = valid && closest_camera<MAXC, FEAT>(S, M, nchunks, cam, d, h);
             // shading inputs (Scene.h:147-154); misses carry harmless placeholders
             const d3 hp = cam + d * h.t;
