@@ -346,6 +346,20 @@ __device__ __forceinline__ void plane_t(double num, double denom, int p, bool& f
     }
 }
 
+// plane_t through the division core for a camera-ray plane whose numerator passed the
+// prologue's test (2^-900 ≤ |num| ≤ 2^400, |n|₁ ≤ 2^90): with 1e-6 < |denom| ≤ 2^91 every
+// operand is inside div_core's range, so t has the bits of num / denom.
+__device__ __forceinline__ void plane_t_core(double num, double denom, int p, bool& found,
+                                             double& best, int& prim) {
+    if (!(fabs(denom) > 1e-6)) return;
+    const double t = div_core(num, denom, rcp_refined(denom));
+    if (t >= 0.0 && (!found || t < best)) {
+        found = true;
+        best = t;
+        prim = p;
+    }
+}
+
 template <int FEAT>
 __device__ __forceinline__ void triangles(const PacketScene& S, d3 o, d3 d, bool& found,
                                           double& best, int& prim) {
@@ -411,7 +425,9 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
     }
     for (int i = 0; i < S.np; ++i) {
         const double* p = S.pl + kPlStride * i;
-        plane_t(p[6], dot(mk(p[3], p[4], p[5]), d), S.ns + i, found, best, prim);
+        const double denom = dot(mk(p[3], p[4], p[5]), d);
+        if (p[7] != 0.0) plane_t_core(p[6], denom, S.ns + i, found, best, prim);  // uniform
+        else plane_t(p[6], denom, S.ns + i, found, best, prim);
     }
     triangles<FEAT>(S, o, d, found, best, prim);
     h.t = best;
@@ -668,7 +684,9 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
         for (int k = 0; k < 6; ++k) o[k] = p[k];
         // camera-ray numerator of Plane::Intersect (Shape.h:152-153)
         o[6] = dot(mk(p[0], p[1], p[2]) - cam, mk(p[3], p[4], p[5]));
-        o[7] = 0.0;
+        // 1 when camera rays may divide it through the core (plane_t_core)
+        const double n1 = fabs(p[3]) + fabs(p[4]) + fabs(p[5]);
+        o[7] = fabs(o[6]) >= 0x1p-900 && fabs(o[6]) <= 0x1p400 && n1 <= 0x1p90 ? 1.0 : 0.0;
     }
     for (int i = tid; i < kLtStride * nl; i += kWgThreads) s_lt[i] = P.lt[i];
     __syncthreads();
