@@ -348,6 +348,40 @@ def test_edge_large_scene_bypasses_lds(ctx, oracle):
     assert np.array_equal(out["hdr64"], oracle.render(sc)[0])
 
 
+@pytest.mark.parametrize("scale", [1e150, 1e-100, 1e-160])
+def test_edge_out_of_core_range_vectors(ctx, oracle, scale):
+    """Lights and spheres at magnitudes where v·v leaves [2^-78, 2^120] (light vectors, hit
+    normals) mixed with ordinary ones in the same waves: the exact lowering takes those lanes
+    (rt_device.hpp), and the image is still bit-identical."""
+    sc = _scene(96, 54)
+    sc.add_sphere((0, 0, 5), 3.0, Material((0.8, 0.3, 0.3)))
+    sc.add_sphere((-6, 2, 8), 2.0, Material((0.3, 0.8, 0.3)))
+    sc.add_sphere((5 * scale, 3 * scale, 40 * scale), 4 * scale, Material((0.3, 0.3, 0.9)))
+    sc.add_plane((0, -4, 0), (0, 1, 0), Material((0.7, 0.7, 0.7)))
+    sc.add_light((0, 10, -5), (1, 1, 1), 150)
+    sc.add_light((0.0, 3.0 + 2 * scale, 5.0), (1, 0.5, 0.5), 20)   # zero x: exact zero components
+    sc.add_light((2 * scale, 2 * scale, -3 * scale), (0.5, 0.5, 1), 80 * scale * scale)
+    out = _render(ctx, sc, hdr64=True, stats=True)
+    ref, nt, ns = oracle.render(sc)
+    assert np.array_equal(out["hdr64"], ref)
+    assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)
+
+
+@pytest.mark.parametrize("offset", [0.0, 1e-300, -1e-200, 1e-13])
+def test_edge_camera_on_or_near_a_plane(ctx, oracle, offset):
+    """Planes through (or within a denormal distance of) the camera give camera-ray numerators
+    outside the plane core's range: those planes take the exact division (rt_packet.hip
+    plane_t); tilted normals give zero / tiny components."""
+    sc = _scene(80, 40)
+    sc.add_plane((0, offset, -25), (0, 1, 0), Material((0.6, 0.6, 0.6)))  # camera at y = 0
+    sc.add_plane((0, -5, 0), (0.0, 1.0, 1e-310), Material((0.5, 0.7, 0.5)))
+    sc.add_plane((0, 0, 30), (0.3, -0.2, -1.0), Material((0.4, 0.4, 0.8)))
+    sc.add_sphere((1, 1, 6), 2.5, Material((0.9, 0.4, 0.2)))
+    sc.add_light((0, 8, 0), (1, 1, 1), 200)
+    out = _render(ctx, sc, hdr64=True)
+    assert np.array_equal(out["hdr64"], oracle.render(sc)[0])
+
+
 def test_invalid_arguments_raise(ctx):
     sc = make_config("c2", 32, 16)
     ds = ctx.scene(sc)
