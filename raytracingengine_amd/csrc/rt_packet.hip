@@ -209,21 +209,26 @@ __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 axis, 
     return M;
 }
 
-// Shadow packet: origins inside ball (c, R), every ray ends at a light inside ball (L, RL);
-// the segments lie in the capsule of radius max(R, RL) around [c, L].  The squared distance
+// Shadow packet: origins inside ball (c, R), every ray aims at a light inside ball (L, RL).
+// The segments [so, lpos] lie in the capsule of radius max(R, RL) around [c, L]; the traced
+// rays do not quite follow them: directLightning takes the direction from the hit point P
+// (L = (lpos − P)/dist) but starts the ray at so = P + n·bias, so the point at parameter t is
+// so + (t/dist)·(lpos − so) + (t/dist)·n·bias, within bias·|n| of its segment for every
+// t ≤ maxDist = dist − bias.  The capsule radius carries that bias (a sphere grazed by the
+// ray but not by the segment is kept).  The squared distance
 // from C to the segment carries < 1.5e-6·(|C−c|² + |L−c|²) of FP32 error (any of the three
 // branches, including a branch chosen wrongly next to a boundary where they meet
 // continuously), against a slack of 2e-5·(|C−c|² + |L−c|²).
 template <int MAXC>
 __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, float R, d3 L,
-                                                    double RL) {
+                                                    double RL, double bias) {
     Masks<MAXC> M;
     const int lane = threadIdx.x & 63;
     const float sx = static_cast<float>(L.x - c.x), sy = static_cast<float>(L.y - c.y),
                 sz = static_cast<float>(L.z - c.z);
     const float sl2 = dot3f(sx, sy, sz, sx, sy, sz);
     const float inv_sl2 = 1.0f / sl2;  // wave-uniform; only read when sl2 > 0
-    const float Rc = fmaxf(R, f32_up(RL));
+    const float Rc = fmaxf(R, f32_up(RL)) + f32_up(fabs(bias)) * 1.001f;  // |n| ≤ 1 + 2ε
 #pragma unroll
     for (int ch = 0; ch < MAXC; ++ch) {
         const int k = ch * 64 + lane;
@@ -600,7 +605,7 @@ __device__ __forceinline__ int pk_occlusion(const PacketScene& S, const Masks<MA
 // radius keep every sphere.
 template <int MAXC>
 __device__ __forceinline__ Masks<MAXC> shadow_masks(const PacketScene& S, bool casting_lane, d3 so,
-                                                    d3 lcenter, double lrad) {
+                                                    d3 lcenter, double lrad, double bias) {
     const uint64_t casting = __ballot(casting_lane);
     if (!casting) return all_candidates<MAXC>(S.ns);
     const bool bad = casting_lane && !(isfinite(so.x) && isfinite(so.y) && isfinite(so.z));
@@ -613,7 +618,7 @@ __device__ __forceinline__ Masks<MAXC> shadow_masks(const PacketScene& S, bool c
     }
     const float R = wave_red<1>(r_lane);
     return __ballot(bad) || !isfinite(R) ? all_candidates<MAXC>(S.ns)
-                                         : cull_capsule<MAXC>(S, c, R, lcenter, lrad);
+                                         : cull_capsule<MAXC>(S, c, R, lcenter, lrad, bias);
 }
 
 // One light of directLightning (Scene.h:86-124) for the whole wave: every lane calls it
@@ -633,7 +638,7 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     const d3 so = P + n * bias;
     const uint64_t casting = __ballot(need);
     if (!casting) return;  // no lane casts this shadow ray (uniform)
-    const Masks<MAXC> M = pre ? *pre : shadow_masks<MAXC>(S, need, so, lcenter, lrad);
+    const Masks<MAXC> M = pre ? *pre : shadow_masks<MAXC>(S, need, so, lcenter, lrad, bias);
     if (!need) return;
     if (COUNT) cnt.shadow++;
     const int occ = pk_occlusion<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
@@ -807,7 +812,7 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
                     const d3 E = mk(P.al_E[0], P.al_E[1], P.al_E[2]);
                     // one packet cull for all samples: every sample's casting lanes are hit
                     // lanes with this origin, and every sample point is in (al_c, al_r)
-                    const Masks<MAXC> Ma = shadow_masks<MAXC>(S, hit, hp + n * bias, al_c, al_r);
+                    const Masks<MAXC> Ma = shadow_masks<MAXC>(S, hit, hp + n * bias, al_c, al_r, bias);
                     for (int q = 0; q < P.al_samples; ++q) {
                         const double r1 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q));
                         const double r2 =

@@ -382,6 +382,42 @@ def test_edge_camera_on_or_near_a_plane(ctx, oracle, offset):
     assert np.array_equal(out["hdr64"], oracle.render(sc)[0])
 
 
+def _grazing_shadow_scene(gap):
+    """1×1 image (all 64 lanes of the wave trace the same pixel, so the shadow packet's origin
+    ball has radius 0) of a floor point lit by a light 0.14 away; a sphere of radius 0.01 sits
+    `gap` beyond the segment [so, light] on the side the traced shadow ray deviates to.  The
+    ray starts at so = P + n·bias but aims along (light − P), so near the light end it runs
+    ~6e-4 off that segment (rt_packet.hip cull_capsule): with gap = 4e-4 it still passes 2e-4
+    inside the sphere, and the reference shades the pixel black."""
+    cam = np.array([0.0, 5.0, 0.0])
+    f = 5.0
+    d = np.array([-0.5, 0.5, cam[2] + f]) - cam    # the 1×1 image's ray (Math.h:99-121)
+    d /= np.linalg.norm(d)
+    P = cam + d * (cam[1] / -d[1])                  # on the floor y = 0
+    so = P + np.array([0.0, 1e-3, 0.0])             # + n·bias
+    light = P + np.array([0.1, 0.1, 0.0])
+    u = (light - so) / np.linalg.norm(light - so)
+    w = np.array([0.0, 1.0, 0.0]) - u[1] * u
+    w /= np.linalg.norm(w)
+    r = 0.01
+    sc = SceneData(Camera(tuple(cam), f, 1, 1, 0.0, 200.0, 1))
+    sc.add_plane((0, 0, 0), (0, 1, 0), Material((0.8, 0.8, 0.8)))
+    sc.add_sphere(tuple(so + 0.12 * u + (r + gap) * w), r, Material((0.9, 0.2, 0.2)))
+    sc.add_light(tuple(light), (1, 1, 1), 1.0)
+    return sc
+
+
+@pytest.mark.parametrize("gap", [4e-4, 5e-2])
+def test_edge_shadow_ray_grazing_near_the_light(ctx, oracle, gap):
+    """The shadow packet's cull covers the traced ray, not only the segment it aims at."""
+    sc = _grazing_shadow_scene(gap)
+    ref, nt, ns = oracle.render(sc)
+    assert (ref == 0).all() == (gap < 1e-3)          # blocked only by the grazed sphere
+    out = _render(ctx, sc, hdr64=True, stats=True)
+    assert np.array_equal(out["hdr64"], ref)
+    assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)
+
+
 def test_invalid_arguments_raise(ctx):
     sc = make_config("c2", 32, 16)
     ds = ctx.scene(sc)
