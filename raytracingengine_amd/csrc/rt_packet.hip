@@ -670,6 +670,7 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
     double* s_pre = s_rad + ns;
     double* s_pl = s_pre + 4 * ns;
     double* s_lt = s_pl + kPlStride * np;
+    double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
     const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     for (int i = tid; i < kSphStride * ns; i += kWgThreads) s_sph[i] = P.sph[i];
     for (int i = tid; i < ns; i += kWgThreads) {
@@ -692,6 +693,19 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
         // 1 when camera rays may divide it through the core (plane_t_core)
         const double n1 = fabs(p[3]) + fabs(p[4]) + fabs(p[5]);
         o[7] = fabs(o[6]) >= 0x1p-900 && fabs(o[6]) <= 0x1p400 && n1 <= 0x1p90 ? 1.0 : 0.0;
+        // Shading normal of a camera-ray hit on this plane (Scene.h:147-154 then directLightning's
+        // normalize, Scene.h:81).  A hit has t = num/denom ≥ 0 with 2^-900 ≤ |num| (no underflow
+        // to ±0) and |denom| > 1e-6, so sign(denom) = sign(num); with |n|₁ ≤ 2 both n·d and the
+        // reference's n·normalize(d) are within 5ε·|n|₁ ≪ 1e-6 of the exact n·d, so frontFace
+        // (n·normalize(d) < 0) is num < 0 for every camera ray that hits the plane, and the
+        // normal is unit(num < 0 ? n : −n): the same for the whole frame.
+        const d3 pn = mk(p[3], p[4], p[5]);
+        const d3 un = unit(o[6] < 0.0 ? pn : -pn);
+        double* q = s_pln + 4 * i;
+        q[0] = un.x;
+        q[1] = un.y;
+        q[2] = un.z;
+        q[3] = o[7] != 0.0 && n1 <= 2.0 ? 1.0 : 0.0;
     }
     for (int i = tid; i < kLtStride * nl; i += kWgThreads) s_lt[i] = P.lt[i];
     __syncthreads();
@@ -775,26 +789,42 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
             const bool hit = valid && closest_camera<MAXC, FEAT>(S, M, nchunks, cam, d, h);
             // shading inputs (Scene.h:147-154); misses carry harmless placeholders
             const d3 hp = cam + d * h.t;
-            const d3 gn = hit ? pk_normal(S, h, hp) : mk(0.0, 1.0, 0.0);
-            // frontFace = n·normalize(d) < 0 (Scene.h:148-150).  d is a unit vector (or zero),
-            // so normalize(d) = d/l·(1+δ) with l = 1 ± 4ε and |δ| ≤ ε; both dot products are
-            // within 5ε·S of their exact values, S = Σ|n_i·d_i| — when |n·d| > 1e-14·S they have
-            // the same sign, and the second normalize (3 divisions) is only needed otherwise.
             // `view` is only read by the Blinn-Phong term.
-            bool front;
             d3 view = mk(0.0, 0.0, 0.0);
+            d3 inc = mk(0.0, 0.0, 0.0);
             if constexpr ((FEAT & kFeatSpec) != 0) {
-                const d3 inc = unit(d);
-                front = dot(gn, inc) < 0.0;
+                inc = unit(d);
                 view = -inc;
-            } else {
-                const double nd = dot(gn, d);
-                const double sabs = fabs(gn.x * d.x) + fabs(gn.y * d.y) + fabs(gn.z * d.z);
-                if (fabs(nd) > 1e-14 * sabs && sabs > 1e-200) front = nd < 0.0;
-                else front = dot(gn, unit(d)) < 0.0;
             }
-            const d3 n0 = front ? gn : -gn;
-            const d3 n = unit(n0);  // directLightning's own normalize (Scene.h:81)
+            // planes: the frame-constant oriented normal of the prologue (s_pln); misses: unused
+            d3 n = mk(0.0, 1.0, 0.0);
+            bool known = !hit;
+            if (hit && h.prim >= ns && h.prim < ns + np) {
+                const double* q = s_pln + 4 * (h.prim - ns);
+                if (q[3] != 0.0) {
+                    n = mk(q[0], q[1], q[2]);
+                    known = true;
+                }
+            }
+            if (!known) {
+                const d3 gn = pk_normal(S, h, hp);
+                // frontFace = n·normalize(d) < 0 (Scene.h:148-150).  d is a unit vector (or
+                // zero), so normalize(d) = d/l·(1+δ) with l = 1 ± 4ε and |δ| ≤ ε; both dot
+                // products are within 5ε·S of their exact values, S = Σ|n_i·d_i| — when
+                // |n·d| > 1e-14·S they have the same sign, and the second normalize (3
+                // divisions) is only needed otherwise.
+                bool front;
+                if constexpr ((FEAT & kFeatSpec) != 0) {
+                    front = dot(gn, inc) < 0.0;
+                } else {
+                    const double nd = dot(gn, d);
+                    const double sabs = fabs(gn.x * d.x) + fabs(gn.y * d.y) + fabs(gn.z * d.z);
+                    if (fabs(nd) > 1e-14 * sabs && sabs > 1e-200) front = nd < 0.0;
+                    else front = dot(gn, unit(d)) < 0.0;
+                }
+                const d3 n0 = front ? gn : -gn;
+                n = unit(n0);  // directLightning's own normalize (Scene.h:81)
+            }
             d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
             for (int l = 0; l < nl; ++l) {
                 const double* lp = S.lt + kLtStride * l;
@@ -878,7 +908,8 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
 
 size_t packet_lds_bytes(int ns, int np, int nl) {
     return sizeof(double) * (static_cast<size_t>(kSphStride + 1 + 4 + 4) * ns +
-                             static_cast<size_t>(kPlStride) * np + static_cast<size_t>(kLtStride) * nl);
+                             static_cast<size_t>(kPlStride + 4) * np +
+                             static_cast<size_t>(kLtStride) * nl);
 }
 
 int packet_max_spheres() { return 16 * 64; }
