@@ -603,22 +603,37 @@ __device__ __forceinline__ int pk_occlusion(const PacketScene& S, const Masks<MA
 // the first such lane's origin (exact), radius = the wave maximum of the distances in FP32
 // rounded up; every segment ends in the light's ball (lcenter, lrad); non-finite origins or
 // radius keep every sphere.
+struct OriginBall {
+    d3 c;
+    float R;
+    bool ok;  // wave-uniform: some lane casts, every origin finite, R finite
+};
+__device__ __forceinline__ OriginBall origin_ball(bool casting_lane, d3 so) {
+    OriginBall B;
+    const uint64_t casting = __ballot(casting_lane);
+    B.c = mk(0.0, 0.0, 0.0);
+    B.R = 0.0f;
+    B.ok = false;
+    if (!casting) return B;
+    const bool bad = casting_lane && !(isfinite(so.x) && isfinite(so.y) && isfinite(so.z));
+    B.c = lane_d3(so, __builtin_ctzll(casting));
+    float r_lane = 0.0f;
+    if (casting_lane) {  // |so − c| in FP32, rounded up (FP64 differences, 5e-7 rel. error)
+        const float dx = static_cast<float>(so.x - B.c.x), dy = static_cast<float>(so.y - B.c.y),
+                    dz = static_cast<float>(so.z - B.c.z);
+        r_lane = sqrt_f32(dot3f(dx, dy, dz, dx, dy, dz)) * (1.0f + 1e-5f);
+    }
+    B.R = wave_red<1>(r_lane);
+    B.ok = !__ballot(bad) && isfinite(B.R);
+    return B;
+}
+
 template <int MAXC>
 __device__ __forceinline__ Masks<MAXC> shadow_masks(const PacketScene& S, bool casting_lane, d3 so,
                                                     d3 lcenter, double lrad, double bias) {
-    const uint64_t casting = __ballot(casting_lane);
-    if (!casting) return all_candidates<MAXC>(S.ns);
-    const bool bad = casting_lane && !(isfinite(so.x) && isfinite(so.y) && isfinite(so.z));
-    const d3 c = lane_d3(so, __builtin_ctzll(casting));
-    float r_lane = 0.0f;
-    if (casting_lane) {  // |so − c| in FP32, rounded up (FP64 differences, 5e-7 rel. error)
-        const float dx = static_cast<float>(so.x - c.x), dy = static_cast<float>(so.y - c.y),
-                    dz = static_cast<float>(so.z - c.z);
-        r_lane = sqrt_f32(dot3f(dx, dy, dz, dx, dy, dz)) * (1.0f + 1e-5f);
-    }
-    const float R = wave_red<1>(r_lane);
-    return __ballot(bad) || !isfinite(R) ? all_candidates<MAXC>(S.ns)
-                                         : cull_capsule<MAXC>(S, c, R, lcenter, lrad, bias);
+    const OriginBall B = origin_ball(casting_lane, so);
+    return B.ok ? cull_capsule<MAXC>(S, B.c, B.R, lcenter, lrad, bias)
+                : all_candidates<MAXC>(S.ns);
 }
 
 // One light of directLightning (Scene.h:86-124) for the whole wave: every lane calls it
@@ -842,7 +857,22 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
                     const d3 E = mk(P.al_E[0], P.al_E[1], P.al_E[2]);
                     // one packet cull for all samples: every sample's casting lanes are hit
                     // lanes with this origin, and every sample point is in (al_c, al_r)
-                    const Masks<MAXC> Ma = shadow_masks<MAXC>(S, hit, hp + n * bias, al_c, al_r, bias);
+                    const OriginBall B = origin_ball(hit, hp + n * bias);
+                    const Masks<MAXC> Ma = B.ok ? cull_capsule<MAXC>(S, B.c, B.R, al_c, al_r, bias)
+                                                : all_candidates<MAXC>(ns);
+                    // When that leaves many candidates (a wide light seen past many spheres),
+                    // each sample gets its own capsule: sample q lies in stratum cell
+                    // (q mod k, q div k), a parallelogram of half-diagonal ≤ (|u|+|v|)/2k
+                    // around the cell centre (plus an absolute term for the rounding of the
+                    // sample and centre positions); its mask is ANDed with the shared one.
+                    int cand = 0;
+#pragma unroll
+                    for (int c = 0; c < MAXC; ++c) cand += __builtin_popcountll(Ma.m[c]);
+                    const bool per_cell = B.ok && cand > 4;
+                    const double cell_r =
+                        ((0.5 * (length(eu) + length(ev))) / k) * (1.0 + kCullRel) +
+                        1e-12 * (fabs(corner.x) + fabs(corner.y) + fabs(corner.z) + fabs(eu.x) +
+                                 fabs(eu.y) + fabs(eu.z) + fabs(ev.x) + fabs(ev.y) + fabs(ev.z));
                     for (int q = 0; q < P.al_samples; ++q) {
                         const double r1 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q));
                         const double r2 =
@@ -850,8 +880,17 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
                         const double fu = (static_cast<double>(q % P.al_k) + r1) / k;
                         const double fv = (static_cast<double>(q / P.al_k) + r2) / k;
                         const d3 lpos = (corner + eu * fu) + ev * fv;
+                        Masks<MAXC> Mq = Ma;
+                        if (per_cell) {  // uniform
+                            const double cu = (static_cast<double>(q % P.al_k) + 0.5) / k;
+                            const double cv = (static_cast<double>(q / P.al_k) + 0.5) / k;
+                            const Masks<MAXC> Mc = cull_capsule<MAXC>(
+                                S, B.c, B.R, (corner + eu * cu) + ev * cv, cell_r, bias);
+#pragma unroll
+                            for (int c = 0; c < MAXC; ++c) Mq.m[c] &= Mc.m[c];
+                        }
                         pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, lpos, E, al_c, al_r,
-                                                    bias, nchunks, diff, spec, cnt, &Ma);
+                                                    bias, nchunks, diff, spec, cnt, &Mq);
                     }
                 }
             }
