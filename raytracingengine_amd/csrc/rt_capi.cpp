@@ -103,6 +103,19 @@ struct rt_scene {
     rt_area_light area{};
     size_t off_bvh = 0, off_bvh_tri = 0;  // triangle BVH, when bvh_nodes > 0
     int32_t bvh_nodes = 0;
+    // Packet-kernel LDS images, one per camera position this scene was rendered from (the
+    // image depends on the spheres, planes, point lights and the camera position only).  An
+    // entry is written once, by packet_image_kernel on the stream of the render that created
+    // it; renders on other streams wait for its event until it has completed.  Never rewritten
+    // or freed before the scene, so a launch in flight never sees it change.
+    struct PkImage {
+        double cam[3];
+        DeviceBuffer buf;
+        hipEvent_t ready = nullptr;
+        hipStream_t stream = nullptr;
+        bool done = false;
+    };
+    mutable std::vector<PkImage> pk_images;
 };
 
 namespace {
@@ -258,6 +271,41 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
     return RT_OK;
 }
 
+// The packet kernel's LDS image for this scene and camera (p.pk_image): looked up by camera
+// position, formed by one setup launch the first time, then copied by every workgroup instead of
+// being recomputed per workgroup.  Past kMaxPkImages cameras the kernel forms it in LDS itself.
+constexpr size_t kMaxPkImages = 16;
+rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
+    for (auto& im : sc->pk_images) {
+        if (std::memcmp(im.cam, p.cam_pos, sizeof im.cam) != 0) continue;
+        if (!im.done && im.stream != ctx->stream) {
+            const hipError_t q = hipEventQuery(im.ready);
+            if (q == hipSuccess) im.done = true;
+            else if (q == hipErrorNotReady) RT_HIP(hipStreamWaitEvent(ctx->stream, im.ready, 0));
+            else return hip_fail(q, "hipEventQuery");
+        }
+        p.pk_image = static_cast<const double*>(im.buf.ptr);
+        return RT_OK;
+    }
+    if (sc->pk_images.size() >= kMaxPkImages) return RT_OK;
+    sc->pk_images.emplace_back();
+    rt_scene::PkImage& im = sc->pk_images.back();
+    std::memcpy(im.cam, p.cam_pos, sizeof im.cam);
+    im.stream = ctx->stream;
+    hipError_t e = im.buf.ensure(packet_lds_bytes(p.ns, p.np, p.nl));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&im.ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = launch_packet_image(p, static_cast<double*>(im.buf.ptr), ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(im.ready, ctx->stream);
+    if (e != hipSuccess) {
+        im.buf.release();
+        if (im.ready) (void)hipEventDestroy(im.ready);
+        sc->pk_images.pop_back();
+        return hip_fail(e, "packet image setup");
+    }
+    p.pk_image = static_cast<const double*>(im.buf.ptr);
+    return RT_OK;
+}
+
 rt_status enqueue(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
                   const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr) {
     TraceParams p;
@@ -293,6 +341,10 @@ rt_status enqueue(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
     const bool packet = path == kPathDirect && !(flags & RT_FLAG_GENERIC_KERNEL) &&
                         p.ns <= packet_max_spheres() &&
                         packet_lds_bytes(p.ns, p.np, p.nl) <= ctx->lds_limit;
+    if (packet) {
+        st = packet_image(ctx, sc, p);
+        if (st != RT_OK) return st;
+    }
     auto launch = [&](const TraceParams& q, bool count) {
         return packet ? launch_packet_direct(q, count, sc->max_specular > 0.0, ctx->stream)
                       : launch_trace(q, path, count, lds, lds_bytes, ctx->stream);
@@ -553,6 +605,10 @@ rt_status rt_scene_destroy(rt_scene* sc) {
     DeviceGuard g(sc->ctx->device);
     (void)hipStreamSynchronize(sc->ctx->stream);
     sc->buf.release();
+    for (auto& im : sc->pk_images) {
+        im.buf.release();
+        if (im.ready) (void)hipEventDestroy(im.ready);
+    }
     delete sc;
     return RT_OK;
 }

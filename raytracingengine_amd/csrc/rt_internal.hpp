@@ -69,6 +69,7 @@ struct TraceParams {
     const uint8_t* redo;  // generic kernels: when set, only pixels with a flagged sample run
     const double* bvh;       // triangle BVH nodes (rt_bvh.cpp), or null: test every triangle
     const int32_t* bvh_tri;  // triangle ids in leaf order
+    const double* pk_image;  // packet kernel: LDS image of this scene + camera, or null
 };
 
 // Host: builds the triangle BVH over the uploaded triangle records (kTriStride doubles each).
@@ -86,6 +87,7 @@ hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, si
 hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specular,
                                 hipStream_t stream);
 size_t packet_lds_bytes(int ns, int np, int nl);
+hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t stream);
 int packet_max_spheres();
 hipError_t launch_trace_rays(const TraceParams& p, int path, bool count, const double* rays,
                              size_t n, double* out, hipStream_t stream);

@@ -674,12 +674,21 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     }
 }
 
-template <int MAXC, int FEAT, bool COUNT, bool MULTI>  // MULTI = false: exactly one sample (AA = 1)
-__global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int tid = threadIdx.x;
+// The packet kernel's LDS image of a scene seen from one camera (layout below, 16-byte
+// aligned arrays): spheres, camera-cone terms, culling radii, camera-ray sphere constants,
+// planes with their camera numerators, point lights, camera-ray plane normals.  Formed by each
+// workgroup into LDS, or once per (scene, camera) into HBM by packet_image_kernel and copied.
+__host__ __device__ inline size_t pk_image_bytes(int ns, int np, int nl) {
+    const size_t b = sizeof(double) * (static_cast<size_t>(kSphStride + 1 + 4 + 4) * ns +
+                                       static_cast<size_t>(kPlStride + 4) * np +
+                                       static_cast<size_t>(kLtStride) * nl);
+    return (b + 15) / 16 * 16;
+}
+
+__device__ __forceinline__ void pk_build_image(const TraceParams& P, double* img, int tid,
+                                               int nthreads) {
     const int ns = P.ns, np = P.np, nl = P.nl;
-    double* s_sph = smem;                                         // 32·ns bytes
+    double* s_sph = img;                                          // 32·ns bytes
     float* s_cone = reinterpret_cast<float*>(s_sph + kSphStride * ns);  // 16-byte aligned
     double* s_rad = s_sph + (kSphStride + 4) * ns;
     double* s_pre = s_rad + ns;
@@ -687,8 +696,8 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
     double* s_lt = s_pl + kPlStride * np;
     double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
     const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    for (int i = tid; i < kSphStride * ns; i += kWgThreads) s_sph[i] = P.sph[i];
-    for (int i = tid; i < ns; i += kWgThreads) {
+    for (int i = tid; i < kSphStride * ns; i += nthreads) s_sph[i] = P.sph[i];
+    for (int i = tid; i < ns; i += nthreads) {
         const double* s = P.sph + kSphStride * i;
         s_rad[i] = sqrt(s[3]);  // culling radius (only ever used with a margin)
         cone_terms(s, s_rad[i], cam, s_cone + 8 * i);
@@ -699,7 +708,7 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
         s_pre[4 * i + 2] = oc.z;
         s_pre[4 * i + 3] = dot(oc, oc) - s[3];
     }
-    for (int i = tid; i < np; i += kWgThreads) {
+    for (int i = tid; i < np; i += nthreads) {
         const double* p = P.pl + kPlStride * i;
         double* o = s_pl + kPlStride * i;
         for (int k = 0; k < 6; ++k) o[k] = p[k];
@@ -722,7 +731,31 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
         q[2] = un.z;
         q[3] = o[7] != 0.0 && n1 <= 2.0 ? 1.0 : 0.0;
     }
-    for (int i = tid; i < kLtStride * nl; i += kWgThreads) s_lt[i] = P.lt[i];
+    for (int i = tid; i < kLtStride * nl; i += nthreads) s_lt[i] = P.lt[i];
+
+}
+
+template <int MAXC, int FEAT, bool COUNT, bool MULTI>  // MULTI = false: exactly one sample (AA = 1)
+__global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int tid = threadIdx.x;
+    const int ns = P.ns, np = P.np, nl = P.nl;
+    double* s_sph = smem;                                         // 32·ns bytes
+    float* s_cone = reinterpret_cast<float*>(s_sph + kSphStride * ns);  // 16-byte aligned
+    double* s_rad = s_sph + (kSphStride + 4) * ns;
+    double* s_pre = s_rad + ns;
+    double* s_pl = s_pre + 4 * ns;
+    double* s_lt = s_pl + kPlStride * np;
+    double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
+    const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    if (P.pk_image) {  // the image of this scene and camera, formed once (packet_image_kernel)
+        const float4* src = reinterpret_cast<const float4*>(P.pk_image);
+        float4* dst = reinterpret_cast<float4*>(smem);
+        const int nv = static_cast<int>(pk_image_bytes(ns, np, nl) / 16);
+        for (int i = tid; i < nv; i += kWgThreads) dst[i] = src[i];
+    } else {
+        pk_build_image(P, smem, tid, kWgThreads);
+    }
     __syncthreads();
 
     PacketScene S;
@@ -945,10 +978,15 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
     }
 }
 
-size_t packet_lds_bytes(int ns, int np, int nl) {
-    return sizeof(double) * (static_cast<size_t>(kSphStride + 1 + 4 + 4) * ns +
-                             static_cast<size_t>(kPlStride + 4) * np +
-                             static_cast<size_t>(kLtStride) * nl);
+size_t packet_lds_bytes(int ns, int np, int nl) { return pk_image_bytes(ns, np, nl); }
+
+__global__ __launch_bounds__(256) void packet_image_kernel(TraceParams P, double* img) {
+    pk_build_image(P, img, static_cast<int>(threadIdx.x), 256);
+}
+
+hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t stream) {
+    hipLaunchKernelGGL(packet_image_kernel, dim3(1), dim3(256), 0, stream, p, img);
+    return hipGetLastError();
 }
 
 int packet_max_spheres() { return 16 * 64; }

@@ -447,6 +447,59 @@ def test_invalid_arguments_raise(ctx):
     assert e.value.status == capi.RT_ERR_UNSUPPORTED
 
 
+def _with_camera(sc, k):
+    import copy
+    out = copy.copy(sc)
+    out.camera = Camera((0.7 * k - 6.0, 0.4 * k - 2.0, -25.0 - 0.5 * k), sc.camera.width / 2.0,
+                        sc.camera.width, sc.camera.height, 0.0, 200.0, 1)
+    return out
+
+
+def test_packet_image_per_camera(ctx, oracle):
+    """The packet kernel's LDS image is formed once per (scene, camera position) and copied by
+    every workgroup (rt_capi.cpp packet_image): 20 camera positions on one uploaded scene — the
+    first 16 get cached images, the rest form the image in LDS — then the first ones again
+    (cache hits); every frame equals the oracle's."""
+    base = make_config("c3", 64, 36)
+    ds = ctx.scene(base)
+    try:
+        frames = []
+        for k in range(20):
+            sc = _with_camera(base, k)
+            ds.camera = sc.camera.to_struct()
+            frames.append(ds.render(hdr64=True)["hdr64"])
+            if k in (0, 7, 15, 16, 19):
+                assert np.array_equal(frames[-1], oracle.render(sc)[0])
+        for k in (0, 3, 18):
+            ds.camera = _with_camera(base, k).camera.to_struct()
+            assert np.array_equal(ds.render(hdr64=True)["hdr64"], frames[k])
+    finally:
+        ds.close()
+
+
+def test_packet_image_shared_across_streams(ctx):
+    """A camera first rendered on one stream and at once on another: the second launch waits
+    for the image's setup event (or finds it complete) — both frames equal a synchronous one."""
+    import torch
+    base = make_config("c2", 256, 128)
+    ds = ctx.scene(base)
+    try:
+        ds.camera = _with_camera(base, 5).camera.to_struct()
+        bufs = [torch.empty(128 * 256 * 3, dtype=torch.float64, device="cuda") for _ in range(2)]
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        for buf, s in zip(bufs, streams):
+            ctx.set_stream(s.cuda_stream)
+            ds.render_device(buf.data_ptr(), None, None, capi.default_opts())
+        for s in streams:
+            s.synchronize()
+        ctx.set_stream(None)
+        ref = ds.render(hdr64=True)["hdr64"].reshape(-1)
+        for buf in bufs:
+            assert np.array_equal(buf.cpu().numpy(), ref)
+    finally:
+        ds.close()
+
+
 def test_render_device_into_torch_buffers(ctx):
     import torch
     sc = make_config("c2", 256, 128)
