@@ -37,12 +37,12 @@ constexpr int kPkH = 8;             // pixels per wave, y
 #ifndef RT_PK_WAVES_X
 #define RT_PK_WAVES_X 2
 #endif
-#ifndef RT_PK_WAVES_Y
-#define RT_PK_WAVES_Y 2
-#endif
 constexpr int kWgWavesX = RT_PK_WAVES_X;  // waves per workgroup, x
-constexpr int kWgWavesY = RT_PK_WAVES_Y;  // waves per workgroup, y
-constexpr int kWgThreads = 64 * kWgWavesX * kWgWavesY;
+// Waves per workgroup in y (the WGY template parameter): 1 (128 threads, 16×8 px) while ten
+// workgroups' LDS images fit the CU's 160 KiB — 20 waves, the 5-waves/SIMD budget — else 2
+// (256 threads, 16×16 px: five images, still 20 waves).  Smaller workgroups wait less for their
+// slowest wave (C3 -3 %, C5 -2 %); with C4's 27 KiB image they would halve the occupancy.
+constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr double kCullRel = 1e-4;   // relative inflation of every culling radius
 constexpr double kFarRatio = 1e5;   // |oc|/r beyond which a sphere is never culled
 constexpr double kNoWin = 1.0 + 0x1.0p-40;  // "quotient provably >= best" factor
@@ -735,8 +735,8 @@ __device__ __forceinline__ void pk_build_image(const TraceParams& P, double* img
 
 }
 
-template <int MAXC, int FEAT, bool COUNT, bool MULTI>  // MULTI = false: exactly one sample (AA = 1)
-__global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
+template <int MAXC, int FEAT, bool COUNT, bool MULTI, int WGY>  // MULTI = false: one sample (AA = 1)
+__global__ __launch_bounds__(64 * kWgWavesX * WGY, ((FEAT == 0 || FEAT == kFeatArea) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
     const int ns = P.ns, np = P.np, nl = P.nl;
@@ -752,9 +752,9 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
         const float4* src = reinterpret_cast<const float4*>(P.pk_image);
         float4* dst = reinterpret_cast<float4*>(smem);
         const int nv = static_cast<int>(pk_image_bytes(ns, np, nl) / 16);
-        for (int i = tid; i < nv; i += kWgThreads) dst[i] = src[i];
+        for (int i = tid; i < nv; i += 64 * kWgWavesX * WGY) dst[i] = src[i];
     } else {
-        pk_build_image(P, smem, tid, kWgThreads);
+        pk_build_image(P, smem, tid, 64 * kWgWavesX * WGY);
     }
     __syncthreads();
 
@@ -783,7 +783,7 @@ __global__ __launch_bounds__(kWgThreads, ((FEAT == 0 || FEAT == kFeatArea) && MA
     // workgroups for the partly idle end (C3 -9 %, C5 -1 %, C2/C4 within ±1 %; centre-out and
     // edges-in orders measured worse).
     const uint32_t by = gridDim.y - 1 - blockIdx.y;
-    const uint32_t yl = by * (kPkH * kWgWavesY) + (wave / kWgWavesX) * kPkH + (lane / kPkW);
+    const uint32_t yl = by * (kPkH * WGY) + (wave / kWgWavesX) * kPkH + (lane / kPkW);
     const bool valid = x < P.width && yl < P.rows;
     // lanes past the image edge trace a clamped in-image ray: they take part in the packet
     // reductions (a superset bound is still conservative) and write nothing.
@@ -991,17 +991,23 @@ hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t st
 
 int packet_max_spheres() { return 16 * 64; }
 
-template <int MAXC, int FEAT>
-static void launch_packet_variant(const TraceParams& p, bool count, size_t lds, hipStream_t stream) {
-    const dim3 block(kWgThreads);
+template <int MAXC, int FEAT, int WGY>
+static void launch_packet_shape(const TraceParams& p, bool count, size_t lds, hipStream_t stream) {
+    const dim3 block(64 * kWgWavesX * WGY);
     const dim3 grid((p.width + kPkW * kWgWavesX - 1) / (kPkW * kWgWavesX),
-                    (p.rows + kPkH * kWgWavesY - 1) / (kPkH * kWgWavesY));
+                    (p.rows + kPkH * WGY - 1) / (kPkH * WGY));
     // the single-sample variant keeps no accumulator live across the trace (AA = 1, the
     // reference default for a preview and the bench's configuration); counting passes use the
     // general one
-    if (count) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, true, true>), grid, block, lds, stream, p);
-    else if (p.aa == 1) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, false>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, true>), grid, block, lds, stream, p);
+    if (count) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, true, true, WGY>), grid, block, lds, stream, p);
+    else if (p.aa == 1) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, false, WGY>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, true, WGY>), grid, block, lds, stream, p);
+}
+
+template <int MAXC, int FEAT>
+static void launch_packet_variant(const TraceParams& p, bool count, size_t lds, hipStream_t stream) {
+    if (10 * lds <= kLdsPerCu) launch_packet_shape<MAXC, FEAT, 1>(p, count, lds, stream);
+    else launch_packet_shape<MAXC, FEAT, 2>(p, count, lds, stream);
 }
 
 template <int MAXC>
