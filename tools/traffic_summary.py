@@ -7,7 +7,7 @@ taken as is."""
 import json, sys
 src, dst, config, alg = sys.argv[1], sys.argv[2], sys.argv[3], float(sys.argv[4])
 d = json.load(open(src))
-k = [n for n in d if "packet" in n or "trace_kernel" in n]
+k = [n for n in d if "packet_direct_kernel" in n or "trace_kernel" in n]
 assert len(k) == 1, k
 c = d[k[0]]
 fetch = c["FETCH_SIZE"] * 1024 * 2
