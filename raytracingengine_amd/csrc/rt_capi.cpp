@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -103,8 +104,8 @@ struct rt_scene {
     rt_area_light area{};
     size_t off_bvh = 0, off_bvh_tri = 0;  // triangle BVH, when bvh_nodes > 0
     int32_t bvh_nodes = 0;
-    // Packet-kernel LDS images, one per camera position this scene was rendered from (the
-    // image depends on the spheres, planes, point lights and the camera position only).  An
+    // Packet-kernel LDS images, one per camera position this scene was rendered from more than
+    // once (the image depends on the spheres, planes, point lights and camera position only).  An
     // entry is written once, by packet_image_kernel on the stream of the render that created
     // it; renders on other streams wait for its event until it has completed.  Never rewritten
     // or freed before the scene, so a launch in flight never sees it change.
@@ -116,6 +117,7 @@ struct rt_scene {
         bool done = false;
     };
     mutable std::vector<PkImage> pk_images;
+    mutable std::vector<std::array<double, 3>> pk_seen;  // cameras rendered once, no image yet
 };
 
 namespace {
@@ -272,9 +274,12 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
 }
 
 // The packet kernel's LDS image for this scene and camera (p.pk_image): looked up by camera
-// position, formed by one setup launch the first time, then copied by every workgroup instead of
-// being recomputed per workgroup.  Past kMaxPkImages cameras the kernel forms it in LDS itself.
+// position and formed by one setup launch the SECOND time a camera is rendered, then copied by
+// every workgroup instead of being recomputed per workgroup.  A camera seen once (a moving
+// camera) takes the in-kernel prologue and costs no setup launch; the last kMaxPkSeen such
+// positions are remembered.  Past kMaxPkImages cached cameras the kernel forms it in LDS.
 constexpr size_t kMaxPkImages = 16;
+constexpr size_t kMaxPkSeen = 16;
 rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
     for (auto& im : sc->pk_images) {
         if (std::memcmp(im.cam, p.cam_pos, sizeof im.cam) != 0) continue;
@@ -287,7 +292,17 @@ rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
         p.pk_image = static_cast<const double*>(im.buf.ptr);
         return RT_OK;
     }
+    auto& seen = sc->pk_seen;
+    auto it = std::find_if(seen.begin(), seen.end(), [&](const std::array<double, 3>& c) {
+        return std::memcmp(c.data(), p.cam_pos, sizeof p.cam_pos) == 0;
+    });
+    if (it == seen.end()) {  // first sighting: remember it, no setup launch
+        if (seen.size() >= kMaxPkSeen) seen.erase(seen.begin());
+        seen.push_back({p.cam_pos[0], p.cam_pos[1], p.cam_pos[2]});
+        return RT_OK;
+    }
     if (sc->pk_images.size() >= kMaxPkImages) return RT_OK;
+    seen.erase(it);
     sc->pk_images.emplace_back();
     rt_scene::PkImage& im = sc->pk_images.back();
     std::memcpy(im.cam, p.cam_pos, sizeof im.cam);

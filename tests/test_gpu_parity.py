@@ -456,10 +456,11 @@ def _with_camera(sc, k):
 
 
 def test_packet_image_per_camera(ctx, oracle):
-    """The packet kernel's LDS image is formed once per (scene, camera position) and copied by
-    every workgroup (rt_capi.cpp packet_image): 20 camera positions on one uploaded scene — the
-    first 16 get cached images, the rest form the image in LDS — then the first ones again
-    (cache hits); every frame equals the oracle's."""
+    """The packet kernel's LDS image is formed once per (scene, camera position) on the second
+    render from that camera and then copied by every workgroup (rt_capi.cpp packet_image): 20
+    camera positions on one uploaded scene, each rendered twice (the first render forms the
+    image in LDS, the second creates the cached one; past 16 cameras every render forms it in
+    LDS), then earlier cameras again (cache hits); every frame equals the oracle's."""
     base = make_config("c3", 64, 36)
     ds = ctx.scene(base)
     try:
@@ -467,7 +468,9 @@ def test_packet_image_per_camera(ctx, oracle):
         for k in range(20):
             sc = _with_camera(base, k)
             ds.camera = sc.camera.to_struct()
+            first = ds.render(hdr64=True)["hdr64"]
             frames.append(ds.render(hdr64=True)["hdr64"])
+            assert np.array_equal(first, frames[-1])
             if k in (0, 7, 15, 16, 19):
                 assert np.array_equal(frames[-1], oracle.render(sc)[0])
         for k in (0, 3, 18):
@@ -478,16 +481,17 @@ def test_packet_image_per_camera(ctx, oracle):
 
 
 def test_packet_image_shared_across_streams(ctx):
-    """A camera first rendered on one stream and at once on another: the second launch waits
-    for the image's setup event (or finds it complete) — both frames equal a synchronous one."""
+    """A camera's image created on one stream (its second render there) and used at once on
+    another: the other stream waits for the setup event (or finds it complete) — every frame
+    equals a synchronous one."""
     import torch
     base = make_config("c2", 256, 128)
     ds = ctx.scene(base)
     try:
         ds.camera = _with_camera(base, 5).camera.to_struct()
-        bufs = [torch.empty(128 * 256 * 3, dtype=torch.float64, device="cuda") for _ in range(2)]
+        bufs = [torch.empty(128 * 256 * 3, dtype=torch.float64, device="cuda") for _ in range(3)]
         streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-        for buf, s in zip(bufs, streams):
+        for buf, s in zip(bufs, (streams[0], streams[0], streams[1])):
             ctx.set_stream(s.cuda_stream)
             ds.render_device(buf.data_ptr(), None, None, capi.default_opts())
         for s in streams:
