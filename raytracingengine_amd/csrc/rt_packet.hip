@@ -357,6 +357,9 @@ __device__ __forceinline__ void plane_t(double num, double denom, int p, bool& f
 __device__ __forceinline__ void plane_t_core(double num, double denom, int p, bool& found,
                                              double& best, int& prim) {
     if (!(fabs(denom) > 1e-6)) return;
+    // opposite signs: t = num/denom is negative and nonzero (|num| ≥ 2^-900), so the
+    // reference's t >= 0 rejects it — a whole wave looking away from the plane skips the division
+    if ((num < 0.0) != (denom < 0.0)) return;
     const double t = div_core(num, denom, rcp_refined(denom));
     if (t >= 0.0 && (!found || t < best)) {
         found = true;
