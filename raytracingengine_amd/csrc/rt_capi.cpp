@@ -360,9 +360,12 @@ rt_status enqueue(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
         st = packet_image(ctx, sc, p);
         if (st != RT_OK) return st;
     }
+    // generic kernels without triangle / area-light code for scenes that use neither
+    const bool lean_generic = p.nt == 0 && p.al_samples == 0;
     auto launch = [&](const TraceParams& q, bool count) {
         return packet ? launch_packet_direct(q, count, sc->max_specular > 0.0, ctx->stream)
-                      : launch_trace(q, path, count, lds, lds_bytes, ctx->stream);
+                      : (lean_generic ? lean::launch_trace(q, path, count, lds, lds_bytes, ctx->stream)
+                                      : launch_trace(q, path, count, lds, lds_bytes, ctx->stream));
     };
     // Scenes with refraction trees take the breadth-first TraceRay when the roots fit the arena
     // budget (RTAMD_WF_MB, default 4096 MiB); trees that overflow it are re-rendered per pixel.

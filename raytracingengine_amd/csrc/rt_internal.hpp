@@ -84,6 +84,10 @@ __host__ __device__ inline size_t scene_doubles(const TraceParams& p) {
 
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
                         hipStream_t stream);
+namespace lean {  // rt_trace_lean.hip: the same kernels for scenes without triangles / area light
+hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
+                        hipStream_t stream);
+}
 hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specular,
                                 hipStream_t stream);
 size_t packet_lds_bytes(int ns, int np, int nl);

@@ -18,6 +18,11 @@
 #pragma clang fp contract(off)
 
 namespace rtamd {
+#ifdef RT_LEAN_GENERIC
+// rt_trace_lean.hip: the per-pixel kernels again, without the triangle / BVH and area-light code
+// (rt_trace_common.hpp), for scenes that have neither: fewer registers, C1 / mirror ~5 % faster.
+namespace lean {
+#endif
 
 template <int PATH, bool COUNT, bool LDS, bool LSTK = false>
 __global__ __launch_bounds__(kTileW * kTileH) void trace_kernel(TraceParams P) {
@@ -121,6 +126,10 @@ hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, si
     default: return launch_path<kPathTree>(p, count, lds, lds_bytes, stream);
     }
 }
+
+#ifdef RT_LEAN_GENERIC
+}  // namespace lean
+#else
 
 // ------------------------------------------------------------------ batch ray queries
 __device__ __forceinline__ SceneView global_view(const TraceParams& P) {
@@ -296,4 +305,5 @@ hipError_t launch_debug_vec(const double* v, size_t n, double* out, hipStream_t 
     return hipGetLastError();
 }
 
+#endif  // RT_LEAN_GENERIC
 }  // namespace rtamd

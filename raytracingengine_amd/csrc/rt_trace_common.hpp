@@ -190,6 +190,7 @@ __device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) 
             }
         }
     }
+#ifndef RT_LEAN_GENERIC  // the lean build (rt_trace_lean.hip) serves scenes without triangles
     if (S.bvh) {
         bvh_triangles(S.tri, S.bvh, S.bvh_tri, o, d, found, best, kind, idx);
     } else {
@@ -203,6 +204,7 @@ __device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) 
             }
         }
     }
+#endif
     h.t = best;
     h.kind = kind;
     h.idx = idx;
@@ -451,6 +453,7 @@ __device__ __forceinline__ d3 direct(const SceneView& S, const TraceParams& P, d
         light_term<COUNT, OPQ>(S, hp, n, view, m, mk(l[0], l[1], l[2]), mk(l[3], l[4], l[5]), bias,
                           diff, spec, cnt);
     }
+#ifndef RT_LEAN_GENERIC  // ... and without the area light
     if (P.al_samples > 0) {
         const uint32_t stream = 0x10000u + (sample << 6) + static_cast<uint32_t>(depth);
         const double k = static_cast<double>(P.al_k);
@@ -467,6 +470,7 @@ __device__ __forceinline__ d3 direct(const SceneView& S, const TraceParams& P, d
             light_term<COUNT, OPQ>(S, hp, n, view, m, lp, E, bias, diff, spec, cnt);
         }
     }
+#endif
     return hmul(m.color, diff) + spec * m.specular;
 }
 
