@@ -25,7 +25,7 @@ namespace lean {
 #endif
 
 template <int PATH, bool COUNT, bool LDS, bool LSTK = false>
-__global__ __launch_bounds__(kTileW * kTileH) void trace_kernel(TraceParams P) {
+__global__ __launch_bounds__(kTileW * kTileH, 2) void trace_kernel(TraceParams P) {
     extern __shared__ double smem[];
     const int tid = threadIdx.y * kTileW + threadIdx.x;
     const SceneView S = stage_scene<LDS>(P, smem, tid, kTileW * kTileH);

@@ -50,7 +50,7 @@ __device__ __forceinline__ void level_range(const WfArena& A, int level, uint32_
 }
 
 template <bool TREE, bool LDS>
-__global__ __launch_bounds__(kWfThreads) void wf_level_kernel(TraceParams P, WfArena A,
+__global__ __launch_bounds__(kWfThreads, 2) void wf_level_kernel(TraceParams P, WfArena A,
                                                               int level) {
     extern __shared__ double smem[];
     const SceneView S = stage_scene<LDS>(P, smem, threadIdx.x, kWfThreads);
