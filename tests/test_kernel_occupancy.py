@@ -1,0 +1,59 @@
+"""Register budgets of the built gfx950 kernels (CPU: reads the code objects' metadata).
+
+Occupancy is the lever measured most in DESIGN.md §4: the single-sample packet kernels run at
+5 waves/SIMD (≤ 96 VGPRs + AGPRs) and the generic / breadth-first trace kernels at 2 (≤ 256).
+An unrelated change once pushed the breadth-first level kernel into AGPRs and 1 wave/SIMD
+(glass +35 %); this pins the budgets on the objects `build()` produced."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OBJ = os.path.join(ROOT, "build", "obj")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _kernels(src):
+    obj = os.path.join(OBJ, src + ".o")
+    if not os.path.exists(obj):
+        pytest.skip(f"{obj} not built")
+    tmp = os.path.join(OBJ, "_meta_" + src)
+    os.makedirs(tmp, exist_ok=True)
+    fb, co = os.path.join(tmp, "fatbin"), os.path.join(tmp, "gfx950.o")
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", obj,
+                    os.path.join(tmp, "host.o")], check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True,
+                           capture_output=True, text=True).stdout
+    out = {}
+    for entry in re.split(r"\n  - \.", notes):  # kernel records (argument records are deeper)
+        name = re.search(r"\n    \.name:\s+(\S+)", entry)
+        v = re.search(r"vgpr_count:\s+(\d+)", entry)
+        a = re.search(r"^agpr_count:\s+(\d+)", entry)
+        if name and v and a and "_kernel" in name.group(1):
+            out[name.group(1)] = int(v.group(1)) + int(a.group(1))
+    assert out, "no kernel metadata found"
+    return out
+
+
+def _waves(regs):
+    return min(8, 512 // max(8, -(-regs // 8) * 8))
+
+
+def test_packet_single_sample_kernels_run_at_5_waves():
+    ks = _kernels("rt_packet.hip")
+    # packet_direct_kernel<MAXC, FEAT, COUNT=false, MULTI=false, WGY>, FEAT 0 (lean) or 2 (area)
+    lean = {n: r for n, r in ks.items() if re.search(r"packet_direct_kernelILi[14]ELi[02]ELb0ELb0E", n)}
+    assert len(lean) == 8, sorted(lean)
+    assert all(_waves(r) >= 5 for r in lean.values()), lean
+
+
+@pytest.mark.parametrize("src", ["rt_trace.hip", "rt_trace_lean.hip", "rt_wavefront.hip"])
+def test_generic_trace_kernels_run_at_2_waves(src):
+    ks = _kernels(src)
+    heavy = {n: r for n, r in ks.items() if "trace_kernel" in n or "wf_level_kernel" in n}
+    assert heavy
+    assert all(_waves(r) >= 2 for r in heavy.values()), heavy
