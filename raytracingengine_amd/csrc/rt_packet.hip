@@ -53,7 +53,8 @@ constexpr int kFeatSpec = 1;    // some opaque material has specular > 0: Blinn-
 constexpr int kFeatArea = 2;    // build-defined area light
 constexpr int kFeatTris = 4;    // triangles / models
 constexpr int kFeatJodie = 8;   // Reinhard-Jodie fused tonemap (log/pow)
-constexpr int kFeatAll = 15;
+constexpr int kFeatPlanes = 16; // ≥ 3 planes: shadow packets also cull planes (cull_capsule)
+constexpr int kFeatAll = 31;
 
 // Waves per SIMD the lean variants are compiled for (4 = at most 128 VGPRs).
 #ifndef RT_PACKET_LEAN_WAVES
@@ -126,6 +127,7 @@ struct PkHit {
 template <int MAXC>
 struct Masks {
     uint64_t m[MAXC];
+    uint64_t pm;  // shadow packets: planes 0..63 that may block (bit set), the rest are clear
 };
 
 template <int MAXC>
@@ -136,6 +138,7 @@ __device__ __forceinline__ Masks<MAXC> all_candidates(int ns) {
         const int left = ns - 64 * c;
         M.m[c] = left >= 64 ? ~0ull : (left <= 0 ? 0ull : ((1ull << left) - 1ull));
     }
+    M.pm = ~0ull;
     return M;
 }
 
@@ -206,6 +209,7 @@ __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 axis, 
         }
         M.m[c] = __ballot(keep);
     }
+    M.pm = ~0ull;
     return M;
 }
 
@@ -219,7 +223,7 @@ __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 axis, 
 // from C to the segment carries < 1.5e-6·(|C−c|² + |L−c|²) of FP32 error (any of the three
 // branches, including a branch chosen wrongly next to a boundary where they meet
 // continuously), against a slack of 2e-5·(|C−c|² + |L−c|²).
-template <int MAXC>
+template <int MAXC, int FEAT>
 __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, float R, d3 L,
                                                     double RL, double bias) {
     Masks<MAXC> M;
@@ -255,6 +259,34 @@ __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, 
                    !(vv <= far * far);
         }
         M.m[ch] = __ballot(keep);
+    }
+    // Planes (feature kFeatPlanes, scenes with three or more, where one lane-parallel test costs
+    // less than the per-lane plane tests it saves): a plane with the capsule strictly on one
+    // side — the origin ball and the light ball on the same side by their radii, the rays' bias
+    // offset and 1e-8 of the magnitudes (FP64 rounding, and pk_occlusion's 1e-9 relative
+    // "beyond the light" margin) — meets no ray of the packet within [0, maxDist], so
+    // pk_occlusion would classify it clear for every lane.  |n|₁ bounds |n|₂.  The exact march
+    // (pk_transmittance) still tests every plane.
+    M.pm = ~0ull;
+    if constexpr ((FEAT & kFeatPlanes) != 0) {
+        if (S.np <= 64) {
+            bool keep = true;
+            if (lane < S.np) {
+                const double* q = S.pl + kPlStride * lane;
+                const d3 pn = mk(q[3], q[4], q[5]);
+                const d3 p0 = mk(q[0], q[1], q[2]);
+                const d3 vc = c - p0, vl = L - p0;
+                const double nn = fabs(pn.x) + fabs(pn.y) + fabs(pn.z);
+                const double sc = dot(vc, pn), sl = dot(vl, pn);
+                const double mag = (fabs(vc.x) + fabs(vc.y) + fabs(vc.z) + fabs(vl.x) +
+                                    fabs(vl.y) + fabs(vl.z) + static_cast<double>(R) + RL) * nn;
+                const double off = fabs(bias) * 1.01 * nn + 1e-8 * mag;
+                const double mc = static_cast<double>(R) * 1.001 * nn + off;
+                const double ml = RL * 1.001 * nn + off;
+                keep = !((sc > mc && sl > ml) || (sc < -mc && sl < -ml));
+            }
+            M.pm = __ballot(keep);
+        }
     }
     return M;
 }
@@ -585,6 +617,7 @@ __device__ __forceinline__ int pk_occlusion(const PacketScene& S, const Masks<MA
         }
     }
     for (int i = 0; i < S.np; ++i) {
+        if (i < 64 && ((M.pm >> i) & 1ull) == 0) continue;  // clear for the whole packet (uniform)
         // Plane::Intersect (Shape.h:149-159): t = num / denom, decided without the division:
         // with A = num·sign(denom), B = |denom|, t lies on the side of x that A lies of x·B
         // (1e-9 relative margin ≫ the FP64 rounding of the quotient and the product)
@@ -631,11 +664,11 @@ __device__ __forceinline__ OriginBall origin_ball(bool casting_lane, d3 so) {
     return B;
 }
 
-template <int MAXC>
+template <int MAXC, int FEAT>
 __device__ __forceinline__ Masks<MAXC> shadow_masks(const PacketScene& S, bool casting_lane, d3 so,
                                                     d3 lcenter, double lrad, double bias) {
     const OriginBall B = origin_ball(casting_lane, so);
-    return B.ok ? cull_capsule<MAXC>(S, B.c, B.R, lcenter, lrad, bias)
+    return B.ok ? cull_capsule<MAXC, FEAT>(S, B.c, B.R, lcenter, lrad, bias)
                 : all_candidates<MAXC>(S.ns);
 }
 
@@ -656,7 +689,7 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     const d3 so = P + n * bias;
     const uint64_t casting = __ballot(need);
     if (!casting) return;  // no lane casts this shadow ray (uniform)
-    const Masks<MAXC> M = pre ? *pre : shadow_masks<MAXC>(S, need, so, lcenter, lrad, bias);
+    const Masks<MAXC> M = pre ? *pre : shadow_masks<MAXC, FEAT>(S, need, so, lcenter, lrad, bias);
     if (!need) return;
     if (COUNT) cnt.shadow++;
     const int occ = pk_occlusion<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
@@ -739,7 +772,7 @@ __device__ __forceinline__ void pk_build_image(const TraceParams& P, double* img
 }
 
 template <int MAXC, int FEAT, bool COUNT, bool MULTI, int WGY>  // MULTI = false: one sample (AA = 1)
-__global__ __launch_bounds__(64 * kWgWavesX * WGY, ((FEAT == 0 || FEAT == kFeatArea) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
+__global__ __launch_bounds__(64 * kWgWavesX * WGY, ((FEAT == 0 || FEAT == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
     const int ns = P.ns, np = P.np, nl = P.nl;
@@ -894,7 +927,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, ((FEAT == 0 || FEAT == kFeatA
                     // one packet cull for all samples: every sample's casting lanes are hit
                     // lanes with this origin, and every sample point is in (al_c, al_r)
                     const OriginBall B = origin_ball(hit, hp + n * bias);
-                    const Masks<MAXC> Ma = B.ok ? cull_capsule<MAXC>(S, B.c, B.R, al_c, al_r, bias)
+                    const Masks<MAXC> Ma = B.ok ? cull_capsule<MAXC, FEAT>(S, B.c, B.R, al_c, al_r, bias)
                                                 : all_candidates<MAXC>(ns);
                     // When that leaves many candidates (a wide light seen past many spheres),
                     // each sample gets its own capsule: sample q lies in stratum cell
@@ -920,10 +953,11 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, ((FEAT == 0 || FEAT == kFeatA
                         if (per_cell) {  // uniform
                             const double cu = (static_cast<double>(q % P.al_k) + 0.5) / k;
                             const double cv = (static_cast<double>(q / P.al_k) + 0.5) / k;
-                            const Masks<MAXC> Mc = cull_capsule<MAXC>(
+                            const Masks<MAXC> Mc = cull_capsule<MAXC, FEAT>(
                                 S, B.c, B.R, (corner + eu * cu) + ev * cv, cell_r, bias);
 #pragma unroll
                             for (int c = 0; c < MAXC; ++c) Mq.m[c] &= Mc.m[c];
+                            Mq.pm &= Mc.pm;
                         }
                         pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, lpos, E, al_c, al_r,
                                                     bias, nchunks, diff, spec, cnt, &Mq);
@@ -1020,6 +1054,7 @@ static void launch_packet_maxc(const TraceParams& p, bool count, size_t lds, int
     // and everything
     if (feat == 0) launch_packet_variant<MAXC, 0>(p, count, lds, stream);
     else if (feat == kFeatArea) launch_packet_variant<MAXC, kFeatArea>(p, count, lds, stream);
+    else if (feat == kFeatPlanes) launch_packet_variant<MAXC, kFeatPlanes>(p, count, lds, stream);
     else launch_packet_variant<MAXC, kFeatAll>(p, count, lds, stream);
 }
 
@@ -1032,6 +1067,8 @@ hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specu
     if (p.al_samples > 0) feat |= kFeatArea;
     if (p.nt > 0) feat |= kFeatTris;
     if (p.ldr && p.tonemap == 4) feat |= kFeatJodie;
+    // the plane cull has its own lean variant; combined with other features the general one
+    if (p.np >= 3 && feat == 0) feat = kFeatPlanes;
     if (chunks <= 1) launch_packet_maxc<1>(p, count, lds, feat, stream);
     else if (chunks <= 4) launch_packet_maxc<4>(p, count, lds, feat, stream);
     else launch_packet_maxc<16>(p, count, lds, feat, stream);

@@ -418,6 +418,27 @@ def test_edge_shadow_ray_grazing_near_the_light(ctx, oracle, gap):
     assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)
 
 
+@pytest.mark.parametrize("gap", [0.0, 5e-4, 2e-3, -3e-4])
+def test_edge_plane_cull_light_near_a_plane(ctx, oracle, gap):
+    """Scenes with ≥ 3 planes cull planes per shadow packet (rt_packet.hip cull_capsule,
+    kFeatPlanes): lights on, just in front of and just behind a wall (within the bias of the
+    shadow rays), tilted planes, and origins on the walls themselves — bit-identical images."""
+    sc = _scene(96, 54)
+    sc.add_plane((0, -6, 0), (0, 1, 0), Material((0.8, 0.8, 0.8)))
+    sc.add_plane((0, 0, 14), (0, 0, -1), Material((0.7, 0.8, 0.9)))
+    sc.add_plane((-12, 0, 0), (1, 0.05, 0), Material((0.9, 0.3, 0.3)))
+    sc.add_plane((12, 0, 0), (-1, 0, 0.02), Material((0.3, 0.9, 0.3)))
+    sc.add_sphere((0, -3, 6), 2.5, Material((0.9, 0.6, 0.2)))
+    sc.add_sphere((-6, 1, 10), 1.5, Material((0.2, 0.6, 0.9)))
+    sc.add_light((2, 4, 14 - gap), (1, 1, 1), 120)     # at / in front of / behind the back wall
+    sc.add_light((-12 + gap, 2, 0), (1, 0.8, 0.6), 80)  # at the left wall
+    sc.add_light((0, 8, -5), (1, 1, 1), 150)
+    out = _render(ctx, sc, hdr64=True, stats=True)
+    ref, nt, ns = oracle.render(sc)
+    assert np.array_equal(out["hdr64"], ref)
+    assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)
+
+
 def test_invalid_arguments_raise(ctx):
     sc = make_config("c2", 32, 16)
     ds = ctx.scene(sc)

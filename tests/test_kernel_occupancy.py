@@ -45,9 +45,11 @@ def _waves(regs):
 
 def test_packet_single_sample_kernels_run_at_5_waves():
     ks = _kernels("rt_packet.hip")
-    # packet_direct_kernel<MAXC, FEAT, COUNT=false, MULTI=false, WGY>, FEAT 0 (lean) or 2 (area)
-    lean = {n: r for n, r in ks.items() if re.search(r"packet_direct_kernelILi[14]ELi[02]ELb0ELb0E", n)}
-    assert len(lean) == 8, sorted(lean)
+    # packet_direct_kernel<MAXC, FEAT, COUNT=false, MULTI=false, WGY>, FEAT 0 (lean), 2 (area)
+    # or 16 (plane cull)
+    lean = {n: r for n, r in ks.items()
+            if re.search(r"packet_direct_kernelILi[14]ELi(0|2|16)ELb0ELb0E", n)}
+    assert len(lean) == 12, sorted(lean)
     assert all(_waves(r) >= 5 for r in lean.values()), lean
 
 
