@@ -23,8 +23,8 @@ ARCH = "gfx950"
 
 HIP_FLAGS = ["-O3", "-std=c++20", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
              "-Wall", "-Wno-unused-result"]
-SOURCES = ["rt_trace.hip", "rt_trace_lean.hip", "rt_packet.hip", "rt_wavefront.hip", "rt_capi.cpp",
-           "rt_bvh.cpp"]
+SOURCES = ["rt_trace.hip", "rt_trace_lean.hip", "rt_packet.hip", "rt_packet_area.hip",
+           "rt_wavefront.hip", "rt_capi.cpp", "rt_bvh.cpp"]
 # per-source extra flags: the packet kernel schedules for ILP (measured 1-2 % faster on C1-C5;
 # the generic kernels are not: mesh/glass 1-5 % slower)
 EXTRA_FLAGS = {"rt_packet.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}

@@ -1015,6 +1015,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, ((FEAT == 0 || FEAT == kFeatA
     }
 }
 
+#ifndef RT_PACKET_AREA_TU
 size_t packet_lds_bytes(int ns, int np, int nl) { return pk_image_bytes(ns, np, nl); }
 
 __global__ __launch_bounds__(256) void packet_image_kernel(TraceParams P, double* img) {
@@ -1027,6 +1028,8 @@ hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t st
 }
 
 int packet_max_spheres() { return 16 * 64; }
+#endif
+
 
 template <int MAXC, int FEAT, int WGY>
 static void launch_packet_shape(const TraceParams& p, bool count, size_t lds, hipStream_t stream) {
@@ -1047,13 +1050,27 @@ static void launch_packet_variant(const TraceParams& p, bool count, size_t lds, 
     else launch_packet_shape<MAXC, FEAT, 2>(p, count, lds, stream);
 }
 
+#ifdef RT_PACKET_AREA_TU
+// rt_packet_area.hip: the area-light variants, in their own translation unit so that they are
+// scheduled with the compiler's default strategy (C5 -2 % against max-ilp, which the other
+// variants keep).
+hipError_t launch_packet_area(const TraceParams& p, bool count, size_t lds, int chunks,
+                              hipStream_t stream) {
+    if (chunks <= 1) launch_packet_variant<1, kFeatArea>(p, count, lds, stream);
+    else if (chunks <= 4) launch_packet_variant<4, kFeatArea>(p, count, lds, stream);
+    else launch_packet_variant<16, kFeatArea>(p, count, lds, stream);
+    return hipGetLastError();
+}
+#else
+hipError_t launch_packet_area(const TraceParams& p, bool count, size_t lds, int chunks,
+                              hipStream_t stream);
+
 template <int MAXC>
 static void launch_packet_maxc(const TraceParams& p, bool count, size_t lds, int feat,
                                hipStream_t stream) {
     // three compiled feature sets: lean (the BASELINE C2-C4 shape), lean + area light (C5),
     // and everything
     if (feat == 0) launch_packet_variant<MAXC, 0>(p, count, lds, stream);
-    else if (feat == kFeatArea) launch_packet_variant<MAXC, kFeatArea>(p, count, lds, stream);
     else if (feat == kFeatPlanes) launch_packet_variant<MAXC, kFeatPlanes>(p, count, lds, stream);
     else launch_packet_variant<MAXC, kFeatAll>(p, count, lds, stream);
 }
@@ -1069,10 +1086,13 @@ hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specu
     if (p.ldr && p.tonemap == 4) feat |= kFeatJodie;
     // the plane cull has its own lean variant; combined with other features the general one
     if (p.np >= 3 && feat == 0) feat = kFeatPlanes;
+    // the area-light variants live in rt_packet_area.hip (compiled with the default scheduler)
+    if (feat == kFeatArea) return launch_packet_area(p, count, lds, chunks, stream);
     if (chunks <= 1) launch_packet_maxc<1>(p, count, lds, feat, stream);
     else if (chunks <= 4) launch_packet_maxc<4>(p, count, lds, feat, stream);
     else launch_packet_maxc<16>(p, count, lds, feat, stream);
     return hipGetLastError();
 }
 
+#endif  // RT_PACKET_AREA_TU
 }  // namespace rtamd

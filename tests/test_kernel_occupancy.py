@@ -44,7 +44,7 @@ def _waves(regs):
 
 
 def test_packet_single_sample_kernels_run_at_5_waves():
-    ks = _kernels("rt_packet.hip")
+    ks = {**_kernels("rt_packet.hip"), **_kernels("rt_packet_area.hip")}
     # packet_direct_kernel<MAXC, FEAT, COUNT=false, MULTI=false, WGY>, FEAT 0 (lean), 2 (area)
     # or 16 (plane cull)
     lean = {n: r for n, r in ks.items()
