@@ -40,8 +40,9 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 
 def build_library(force: bool = False, verbose: bool = False) -> str:
+    # the recipe itself is a dependency: a change of HIP_FLAGS / EXTRA_FLAGS / SOURCES rebuilds
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [
-        os.path.join(ROOT, "include", "rt_capi.h")]
+        os.path.join(ROOT, "include", "rt_capi.h"), os.path.abspath(__file__)]
     if not force and not _stale(LIB, deps):
         return LIB
     os.makedirs(OBJ_DIR, exist_ok=True)
@@ -80,7 +81,7 @@ def build_cpp_api(force: bool = False, verbose: bool = False) -> str:
     hdrs = [os.path.join(API_DIR, "rtamd", f) for f in os.listdir(os.path.join(API_DIR, "rtamd"))]
     link = [f"-L{HERE}", "-lrtamd", f"-Wl,-rpath,{HERE}", "-Wl,-rpath,$ORIGIN"]
     cxx = os.environ.get("CXX", "g++")
-    if force or _stale(CPP_LIB, srcs + hdrs + [LIB]):
+    if force or _stale(CPP_LIB, srcs + hdrs + [LIB, os.path.abspath(__file__)]):
         cmd = [cxx, *CPP_FLAGS, "-shared", "-o", CPP_LIB, *srcs, *link]
         if verbose:
             print(" ".join(cmd), flush=True)

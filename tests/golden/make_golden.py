@@ -7,6 +7,7 @@ and the reference's outputs for them.  The reference has no tests or fixtures of
 (SURVEY.md §4), so these are the pins of the oracle.
 
     python tests/golden/make_golden.py          # rewrites tests/golden/*.npz / *.json
+    python tests/golden/make_golden.py --full   # adds the full-size frames (FULL2_SCENES)
 """
 from __future__ import annotations
 
@@ -212,6 +213,49 @@ def main():
     print(json.dumps(sizes))
 
 
+# Full-size frames added in round 2 (``--full``): the BASELINE configs the bench and the scaling
+# runs render, at their own resolution.  HDR: sha256 of the float64 image + a sparse subsample
+# (diagnostics on a mismatch; configs whose shading calls libm pow are compared on the subsample
+# within the pow tolerance).  LDR: sha256 of the bytes of tonemapAll() (7 operators) and
+# tonemap() (ACES) of the reference, RaytracingEngine.cpp:113-135,165-214.
+FULL2_SCENES = {"c2": 64, "c3": 1024, "c4": 4096, "mirror": 256, "glass": 256, "mesh": 256}
+LDR_NAMES = REFAPP_NAMES + ["tonemap_aces"]
+
+
+def full_golden():
+    if not po.ref_available():
+        po.build()
+    meta_path = os.path.join(HERE, "golden_meta.json")
+    with open(meta_path) as fh:
+        meta = json.load(fh)
+    sub_path = os.path.join(HERE, "renders_full_subsample.npz")
+    full = dict(np.load(sub_path))
+    with tempfile.TemporaryDirectory() as td:
+        for name, stride in FULL2_SCENES.items():
+            sc = make_config(name)
+            img, ms, thr = po.ref_render(sc)
+            flat = np.ascontiguousarray(img.reshape(-1, 3))
+            key = f"{name}_full"
+            if name not in full or stride != SUBSAMPLE:
+                full[name if stride == SUBSAMPLE else f"{name}_s{stride}"] = flat[::stride]
+            entry = meta["scenes"].get(key, {})
+            entry.update({"scene_sha256": scene_hash(sc), "width": sc.camera.width,
+                          "height": sc.camera.height,
+                          "image_sha256": hashlib.sha256(flat.tobytes()).hexdigest(),
+                          "subsample_stride": stride})
+            inp, out = os.path.join(td, "px.f64"), os.path.join(td, "px.u8")
+            flat.tofile(inp)
+            run("tonemap", inp, len(flat), out)
+            ldr = np.fromfile(out, np.uint8).reshape(8, len(flat), 3)
+            entry["ldr_sha256"] = {n: hashlib.sha256(ldr[i].tobytes()).hexdigest()
+                                   for i, n in enumerate(LDR_NAMES)}
+            meta["scenes"][key] = entry
+            print(name, f"{ms[0]:.0f} ms on {thr} threads", entry["image_sha256"][:16], flush=True)
+    np.savez_compressed(sub_path, **full)
+    with open(meta_path, "w") as fh:
+        json.dump(meta, fh, indent=1, sort_keys=True)
+
+
 def obj_golden():
     """The reference application's LoadObject (tinyobjloader) on the OBJ fixtures: triangles as
     9 doubles each (oracle/_ref/ref_harness obj)."""
@@ -230,5 +274,7 @@ if __name__ == "__main__":
         refapp_golden()
     elif "--obj" in sys.argv:
         obj_golden()
+    elif "--full" in sys.argv:
+        full_golden()
     else:
         main()

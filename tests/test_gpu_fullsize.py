@@ -1,0 +1,134 @@
+"""Full-size parity of the launches the bench and the scaling runs time, against the UNMODIFIED
+reference's frames (tests/golden/make_golden.py --full: SHA-256 of the reference's float64
+RenderImage() and of the bytes of its tonemapAll()/tonemap(), RaytracingEngine.cpp:113-214).
+
+The bench renders C2 from one static camera, so its timed launches read the per-(scene, camera)
+packet image that the SECOND render creates (rt_capi.cpp packet_image); the first render forms
+the image inside the kernel.  Every test here renders each frame three times from one camera —
+fresh, cache-creating, cached — and pins every render.
+
+Bars: C2-C4 (no libm pow on the path) bit-exact HDR and byte-identical LDR for every operator
+except Reinhard-Jodie (device pow/log within 1 ulp: a handful of one-step byte flips allowed);
+mirror/glass/mesh (Blinn-Phong / Fresnel pow): HDR within 1e-12 on the golden subsample.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from raytracingengine_amd import capi
+from raytracingengine_amd.configs import make_config
+
+pytestmark = pytest.mark.gpu
+
+POW_TOL = 1e-12
+JODIE_MAX_FLIPS = 16
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("name", ["c2", "c3", "c4"])
+def test_full_frame_sha_fresh_cache_creating_cached(ctx, golden, name):
+    """The exact benchmarked launch at full size: float64 HDR + fused Reinhard u8 (the bench's
+    outputs), three renders from one camera, every one equal to the reference's frame."""
+    info = golden["meta"]["scenes"][f"{name}_full"]
+    sc = make_config(name)
+    assert (sc.camera.width, sc.camera.height) == (info["width"], info["height"])
+    ds = ctx.scene(sc)
+    try:
+        for k in range(3):
+            out = ds.render(hdr64=True, tonemap=1)
+            assert _sha(out["hdr64"]) == info["image_sha256"], (name, k)
+            assert _sha(out["ldr"]) == info["ldr_sha256"]["reinhard_simple"], (name, k)
+            del out
+    finally:
+        ds.close()
+
+
+def test_full_c2_float32_framebuffer_and_bytes(ctx, golden):
+    """`bench.py --hdr f32` (the north star's float3 framebuffer): the float32 frame is the
+    reference's float64 frame rounded to float, the bytes are the reference's."""
+    info = golden["meta"]["scenes"]["c2_full"]
+    sc = make_config("c2")
+    ds = ctx.scene(sc)
+    try:
+        for k in range(3):
+            out = ds.render(hdr64=True, hdr32=True, tonemap=1)
+            assert _sha(out["hdr64"]) == info["image_sha256"], k
+            assert np.array_equal(out["hdr32"], out["hdr64"].astype(np.float32)), k
+            assert _sha(out["ldr"]) == info["ldr_sha256"]["reinhard_simple"], k
+    finally:
+        ds.close()
+
+
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_full_frame_all_operators_vs_reference_bytes(ctx, golden, name):
+    """tonemapAll() (7 operators) and tonemap() of the full frame: the fused operator of each
+    render and the standalone rt_tonemap pass both give the reference's bytes."""
+    info = golden["meta"]["scenes"][f"{name}_full"]
+    sc = make_config(name)
+    ds = ctx.scene(sc)
+    try:
+        hdr = None
+        for op, op_name in enumerate(capi.TONEMAPS):
+            out = ds.render(hdr64=hdr is None, tonemap=op)
+            if hdr is None:
+                hdr = out["hdr64"]
+                assert _sha(hdr) == info["image_sha256"]
+            ref_sha = info["ldr_sha256"][op_name]
+            if op_name == "reinhard_jodie":
+                continue  # compared below with the standalone pass
+            assert _sha(out["ldr"]) == ref_sha, op_name
+        planes = ctx.tonemap(hdr, capi.TONEMAP_ALL)
+        for op, op_name in enumerate(capi.TONEMAPS):
+            if op_name == "reinhard_jodie":
+                fused = ds.render(hdr64=False, tonemap=op)["ldr"].reshape(-1, 3)
+                assert np.array_equal(fused, planes[op])
+                continue
+            assert _sha(planes[op]) == info["ldr_sha256"][op_name], op_name
+        assert _sha(ctx.tonemap(hdr, capi.TONEMAPS.index("aces"))) == \
+            info["ldr_sha256"]["tonemap_aces"]
+    finally:
+        ds.close()
+
+
+def test_full_c2_reinhard_jodie_within_one_step(ctx, golden, oracle):
+    """Reinhard-Jodie calls libm pow/log (RaytracingEngine.cpp:150-154): device libm is within
+    1 ulp, so a few bytes may sit one step from the reference's; everything else is identical."""
+    sc = make_config("c2")
+    ds = ctx.scene(sc)
+    try:
+        out = ds.render(hdr64=True, tonemap=capi.TONEMAPS.index("reinhard_jodie"))
+    finally:
+        ds.close()
+    ref = oracle.tonemap(out["hdr64"], capi.TONEMAPS.index("reinhard_jodie"))
+    got = out["ldr"].reshape(-1, 3)
+    diff = np.abs(got.astype(np.int16) - ref.astype(np.int16))
+    assert diff.max() <= 1
+    assert int((diff > 0).sum()) <= JODIE_MAX_FLIPS
+    if int((diff > 0).sum()) == 0:  # the oracle's bytes are the reference's (test_oracle_golden)
+        assert _sha(got) == golden["meta"]["scenes"]["c2_full"]["ldr_sha256"]["reinhard_jodie"]
+
+
+@pytest.mark.parametrize("name", ["mirror", "glass", "mesh"])
+def test_full_frame_pow_scenes_vs_reference_subsample(ctx, golden, name):
+    """Reflection chains (mirror), refraction trees breadth-first (glass) and the triangle BVH
+    (mesh) at full 1920x1080 against the reference's frame: within 1e-12 on a 1-in-256
+    subsample (Blinn-Phong / Fresnel pow), three renders from one camera."""
+    info = golden["meta"]["scenes"][f"{name}_full"]
+    stride = info["subsample_stride"]
+    sub = golden["full"][f"{name}_s{stride}"]
+    sc = make_config(name)
+    ds = ctx.scene(sc)
+    try:
+        for k in range(3):
+            out = ds.render(hdr64=True, tonemap=6)
+            got = out["hdr64"].reshape(-1, 3)[::stride]
+            d = np.abs(got - sub).max()
+            assert d <= POW_TOL, (name, k, d)
+            if _sha(out["hdr64"]) == info["image_sha256"]:
+                assert _sha(out["ldr"]) == info["ldr_sha256"]["aces"]
+    finally:
+        ds.close()

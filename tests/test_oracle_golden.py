@@ -124,3 +124,20 @@ def test_tonemap_bytes_and_curves(golden, oracle):
     # black pixels: luminance operators divide 0/0, ClampVec3's max(0, NaN) gives 0
     assert (k["tonemap_bytes"][:, :16] == 0).all()
     assert np.isnan(k["tonemap_curves"][3, :16]).all()
+
+
+@pytest.mark.parametrize("name", ["c3", "c4", "mirror", "glass", "mesh"])
+def test_full_size_rows_vs_reference_subsample(golden, oracle, name):
+    """The round-2 full-size goldens (make_golden.py --full): oracle rows at the reference's full
+    resolution equal the reference frame's subsample entries that fall in them, bit for bit."""
+    sc = make_config(name)
+    info = golden["meta"]["scenes"][f"{name}_full"]
+    assert _scene_sha(sc) == info["scene_sha256"]
+    stride = info["subsample_stride"]
+    sub = golden["full"][f"{name}_s{stride}"]
+    W, H = sc.camera.width, sc.camera.height
+    for r in (0, H // 3, H // 2 + 1, H - 1):
+        img, _, _ = oracle.render(sc, rows=(r, r + 1))
+        first = -(-r * W // stride)          # subsample entries inside row r
+        idx = np.arange(first * stride, (r + 1) * W, stride)
+        assert np.array_equal(img.reshape(-1, 3)[idx - r * W], sub[idx // stride]), (name, r)
