@@ -42,7 +42,8 @@ typedef enum rt_status {
     RT_ERR_HIP = 2,         /* a HIP runtime call failed (message names the call)           */
     RT_ERR_OOM = 3,         /* device allocation failed                                     */
     RT_ERR_UNSUPPORTED = 4, /* a request outside what this build implements                 */
-    RT_ERR_NO_DEVICE = 5    /* no gfx950 device at the requested ordinal                    */
+    RT_ERR_NO_DEVICE = 5,   /* no gfx950 device at the requested ordinal                    */
+    RT_ERR_RCCL = 6         /* an RCCL call failed (message names the call)                 */
 } rt_status;
 
 /* Material (Shape.h:13-19).  Defaults in the reference: shininess 128, specular 0,
@@ -205,14 +206,64 @@ rt_status rt_render(rt_context* ctx, const rt_scene* scene, const rt_camera* cam
                     uint8_t* ldr_out, rt_stats* stats);
 
 /* One frame on n contexts (one per GPU, each with its own copy of the scene: scenes[i] belongs to
- * ctxs[i]), assembled in the caller's host buffers — Scene::RenderImage over the GPUs of a node
- * from one process.  Context i renders the block-cyclic row set i of n (opts->row_block rows per
- * block, default 16; the row range and row_cycle of opts must be left at the whole image); all
- * contexts run concurrently, then every context's rows are copied to their image rows.  Stats,
- * when requested, are summed over the contexts. */
+ * ctxs[i]), returned in the caller's host buffers — Scene::RenderImage (Scene.h:311-328) over the
+ * GPUs of a node from one process.  Context i renders the block-cyclic row set i of n
+ * (opts->row_block rows per block, default 16; the row range and row_cycle of opts must be left
+ * at the whole image).  Contexts on distinct GPUs: the RCCL path — communicators over their
+ * devices (ncclCommInitAll, created on first use and cached in ctxs[0] until the list changes),
+ * rt_render_gather_all into ctxs[0]'s device, one device-to-host copy per output.  Contexts that
+ * share a GPU (RCCL allows one rank per GPU): each context's rows are copied to their host rows.
+ * Stats, when requested, are summed over the contexts (kernel_ms: the slowest GPU's render). */
 rt_status rt_render_multi(rt_context* const* ctxs, rt_scene* const* scenes, int n,
                           const rt_camera* cam, const rt_render_opts* opts, double* hdr64_out,
                           float* hdr32_out, uint8_t* rgb8_out, rt_stats* stats);
+
+/* ---- Row-tiled frames over the GPUs of a node with ONE RCCL gather ----------
+ * Replaces the pixel loop of Scene::RenderImage (Scene.h:318-325) split by rows: rank r of n
+ * renders the block-cyclic row set r (blocks of opts->row_block rows, default 16, starting at
+ * row r*block and every n*block rows after it), one ncclGather per requested output moves every
+ * rank's rows (padded to the largest rank's) to rank 0 over xGMI, and rank 0 writes them into
+ * image row order in its device framebuffers.  Everything is enqueued on the communicator's
+ * context stream; no host synchronisation. */
+#define RT_COMM_ID_BYTES 128    /* == NCCL_UNIQUE_ID_BYTES                                   */
+#define RT_OUT_HDR64 0x1        /* float64 Vec3 framebuffer (24 B/px)                        */
+#define RT_OUT_HDR32 0x2        /* float32 framebuffer (12 B/px)                             */
+#define RT_OUT_LDR 0x4          /* tonemapped bytes of opts->tonemap (3 B/px)                */
+
+typedef struct rt_comm rt_comm;
+
+typedef struct rt_gather_timing {
+    double render_ms;    /* summed over the timed frames (RT_FLAG_TIME_KERNEL), this rank   */
+    double gather_ms;    /* the ncclGather(s), from the end of this rank's render           */
+    double assemble_ms;  /* rank 0: the gathered rows written into image order              */
+    uint64_t frames;     /* frames timed                                                    */
+    uint32_t rows;       /* rows this rank renders per frame                                */
+    uint32_t max_rows;   /* rows every rank sends (the largest rank's)                      */
+} rt_gather_timing;
+
+/* ncclGetUniqueId: called on one process, the bytes handed to every rank (any transport). */
+rt_status rt_comm_unique_id(uint8_t* id /* RT_COMM_ID_BYTES */);
+/* One rank of an n-rank communicator on ctx's device (ncclCommInitRank): one process per GPU.
+ * Destroy communicators before their contexts. */
+rt_status rt_comm_create(rt_context* ctx, int nranks, int rank, const uint8_t* id, rt_comm** out);
+/* n communicators, one per context, over n DISTINCT devices from one process (ncclCommInitAll);
+ * comms_out[i] is rank i on ctxs[i]. */
+rt_status rt_comm_create_all(rt_context* const* ctxs, int n, rt_comm** comms_out);
+rt_status rt_comm_destroy(rt_comm* comm);
+rt_status rt_comm_info(const rt_comm* comm, int* nranks, int* rank);
+/* Collective: every rank calls it with the same camera, opts and outputs (RT_OUT_* bits).  The
+ * scene belongs to the communicator's context.  On rank 0 the d_* are whole-frame device
+ * framebuffers (W*H*3 elements, image order) for every requested output; elsewhere ignored.
+ * opts->flags RT_FLAG_TIME_KERNEL records the frame's render / gather / assembly times. */
+rt_status rt_render_gather(rt_comm* comm, const rt_scene* scene, const rt_camera* cam,
+                           const rt_render_opts* opts, int outputs, void* d_hdr64,
+                           void* d_hdr32, void* d_ldr);
+/* The same from one process for every rank of an rt_comm_create_all (one ncclGroup). */
+rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, int n,
+                               const rt_camera* cam, const rt_render_opts* opts, int outputs,
+                               void* d_hdr64, void* d_hdr32, void* d_ldr);
+/* Summed frame timings since the last reset (waits for the timed frames to finish). */
+rt_status rt_comm_timing(rt_comm* comm, rt_gather_timing* out, int reset);
 
 /* Asynchronous render into DEVICE buffers on the context's stream (inputs and outputs stay
  * resident in HBM).  Same layouts as rt_render; pointers are device pointers or NULL. */
@@ -251,6 +302,12 @@ rt_status rt_debug_f64_ops(rt_context* ctx, const double* x, const double* y, si
  * sqrt/division cores next to the compiler's exact lowering, so the parity suite can pin them bit
  * for bit.  out: 16*n doubles (layout in rt_trace.hip, debug_vec_kernel). */
 rt_status rt_debug_vec_ops(rt_context* ctx, const double* v, size_t n, double* out);
+
+/* Test hook: rank 0's assembly step alone (gathered [n][max_rows][row_bytes] host buffer ->
+ * image-order [height][row_bytes] host buffer) for row plans the 1-GPU test box cannot run. */
+rt_status rt_debug_assemble_rows(rt_context* ctx, const void* gathered, size_t row_bytes,
+                                 uint32_t height, uint32_t block, uint32_t n, uint32_t max_rows,
+                                 void* image);
 
 #ifdef __cplusplus
 } /* extern "C" */

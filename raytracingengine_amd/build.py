@@ -24,7 +24,10 @@ ARCH = "gfx950"
 HIP_FLAGS = ["-O3", "-std=c++20", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
              "-Wall", "-Wno-unused-result"]
 SOURCES = ["rt_trace.hip", "rt_trace_lean.hip", "rt_packet.hip", "rt_packet_area.hip",
-           "rt_wavefront.hip", "rt_capi.cpp", "rt_bvh.cpp"]
+           "rt_wavefront.hip", "rt_assemble.hip", "rt_capi.cpp", "rt_multi.cpp", "rt_bvh.cpp"]
+# RCCL (multi-GPU frames, rt_multi.cpp).  Inside a PyTorch process the loader reuses torch's
+# librccl.so.1 (same soname, loaded first by capi.load_library), so one RCCL serves both.
+LINK_LIBS = ["-L/opt/rocm/lib", "-lrccl"]
 # per-source extra flags: the packet kernel schedules for ILP (measured 1-2 % faster on C1-C5;
 # the generic kernels are not: mesh/glass 1-5 % slower)
 EXTRA_FLAGS = {"rt_packet.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
@@ -40,26 +43,30 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 
 def build_library(force: bool = False, verbose: bool = False) -> str:
-    # the recipe itself is a dependency: a change of HIP_FLAGS / EXTRA_FLAGS / SOURCES rebuilds
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [
+    # the recipe itself is a dependency: a change of HIP_FLAGS / EXTRA_FLAGS / SOURCES rebuilds.
+    # Objects are rebuilt per source: a source's object is stale when the source, any header
+    # (csrc/*.hpp, include/rt_capi.h) or this recipe is newer.
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))] + [
         os.path.join(ROOT, "include", "rt_capi.h"), os.path.abspath(__file__)]
-    if not force and not _stale(LIB, deps):
-        return LIB
     os.makedirs(OBJ_DIR, exist_ok=True)
     inc = f"-I{os.path.join(ROOT, 'include')}"
     procs, objs = [], []
-    for src in SOURCES:  # one hipcc per source, in parallel
+    for src in SOURCES:  # one hipcc per stale source, in parallel
         obj = os.path.join(OBJ_DIR, src + ".o")
+        objs.append(obj)
+        if not force and not _stale(obj, [os.path.join(CSRC, src)] + headers):
+            continue
         cmd = [HIPCC, *HIP_FLAGS, *EXTRA_FLAGS.get(src, []), inc, "-c", "-o", obj,
                os.path.join(CSRC, src)]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append((cmd, subprocess.Popen(cmd)))
-        objs.append(obj)
     for cmd, p in procs:
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, cmd)
-    cmd = [HIPCC, *HIP_FLAGS, "-shared", "-o", LIB, *objs]
+    if not force and not procs and not _stale(LIB, objs):
+        return LIB
+    cmd = [HIPCC, *HIP_FLAGS, "-shared", "-o", LIB, *objs, *LINK_LIBS]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

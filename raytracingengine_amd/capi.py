@@ -16,9 +16,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # RTAMD_LIB overrides the library path (A/B builds in tools/); default: the in-tree build.
 LIB_PATH = os.environ.get("RTAMD_LIB", os.path.join(HERE, "librtamd.so"))
 
-RT_OK, RT_ERR_INVALID_ARG, RT_ERR_HIP, RT_ERR_OOM, RT_ERR_UNSUPPORTED, RT_ERR_NO_DEVICE = range(6)
+(RT_OK, RT_ERR_INVALID_ARG, RT_ERR_HIP, RT_ERR_OOM, RT_ERR_UNSUPPORTED, RT_ERR_NO_DEVICE,
+ RT_ERR_RCCL) = range(7)
 STATUS_NAMES = {0: "RT_OK", 1: "RT_ERR_INVALID_ARG", 2: "RT_ERR_HIP", 3: "RT_ERR_OOM",
-                4: "RT_ERR_UNSUPPORTED", 5: "RT_ERR_NO_DEVICE"}
+                4: "RT_ERR_UNSUPPORTED", 5: "RT_ERR_NO_DEVICE", 6: "RT_ERR_RCCL"}
 
 TONEMAP_NONE = -1
 TONEMAPS = ["simple", "reinhard_simple", "reinhard_extended", "reinhard_extended_luminance",
@@ -28,13 +29,17 @@ RT_FLAG_COUNT_RAYS = 0x1
 RT_FLAG_TIME_KERNEL = 0x2
 RT_FLAG_GENERIC_KERNEL = 0x4
 RT_FLAG_NO_BVH = 0x8
+RT_OUT_HDR64, RT_OUT_HDR32, RT_OUT_LDR = 0x1, 0x2, 0x4
+RT_COMM_ID_BYTES = 128
 
 # Every symbol include/rt_capi.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED = [
     "rt_last_error", "rt_device_count", "rt_render_opts_default", "rt_context_create",
     "rt_context_destroy", "rt_context_set_stream", "rt_context_synchronize", "rt_scene_create",
     "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
-    "rt_render_multi",
+    "rt_render_multi", "rt_comm_unique_id", "rt_comm_create", "rt_comm_create_all",
+    "rt_comm_destroy", "rt_comm_info", "rt_render_gather", "rt_render_gather_all",
+    "rt_comm_timing", "rt_debug_assemble_rows",
     "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
     "rt_debug_f64_ops", "rt_debug_vec_ops",
 ]
@@ -68,6 +73,14 @@ class Stats(ctypes.Structure):
     _fields_ = [
         ("trace_rays", ctypes.c_uint64), ("shadow_rays", ctypes.c_uint64),
         ("kernel_ms", ctypes.c_double), ("launches", ctypes.c_uint64),
+    ]
+
+
+class GatherTiming(ctypes.Structure):
+    _fields_ = [
+        ("render_ms", ctypes.c_double), ("gather_ms", ctypes.c_double),
+        ("assemble_ms", ctypes.c_double), ("frames", ctypes.c_uint64),
+        ("rows", ctypes.c_uint32), ("max_rows", ctypes.c_uint32),
     ]
 
 
@@ -113,6 +126,16 @@ def load_library(path: str = LIB_PATH):
         "rt_tonemap": [vp, vp, ctypes.c_size_t, i32, vp],
         "rt_debug_f64_ops": [vp, vp, vp, ctypes.c_size_t, vp],
         "rt_debug_vec_ops": [vp, vp, ctypes.c_size_t, vp],
+        "rt_comm_unique_id": [vp],
+        "rt_comm_create": [vp, i32, i32, vp, vp],
+        "rt_comm_create_all": [vp, i32, vp],
+        "rt_comm_destroy": [vp],
+        "rt_comm_info": [vp, vp, vp],
+        "rt_render_gather": [vp, vp, vp, vp, i32, vp, vp, vp],
+        "rt_render_gather_all": [vp, vp, i32, vp, vp, i32, vp, vp, vp],
+        "rt_comm_timing": [vp, vp, i32],
+        "rt_debug_assemble_rows": [vp, vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                   ctypes.c_uint32, ctypes.c_uint32, vp],
     }.items():
         fn = getattr(L, name)
         fn.argtypes = args
@@ -210,6 +233,15 @@ class Context:
         out = np.empty((x.size, 4), np.float64)
         _check(_lib.rt_debug_f64_ops(self._h, x.ctypes.data, y.ctypes.data, x.size,
                                      out.ctypes.data))
+        return out
+
+    def debug_assemble_rows(self, gathered: np.ndarray, height: int, block: int, n: int,
+                            max_rows: int) -> np.ndarray:
+        """rank 0's assembly step alone: gathered uint8 [n, max_rows, row_bytes] -> image rows."""
+        g = np.ascontiguousarray(gathered, np.uint8).reshape(n, max_rows, -1)
+        out = np.empty((height, g.shape[2]), np.uint8)
+        _check(_lib.rt_debug_assemble_rows(self._h, g.ctypes.data, g.shape[2], height, block, n,
+                                           max_rows, out.ctypes.data))
         return out
 
     def debug_vec_ops(self, v: np.ndarray) -> np.ndarray:
@@ -330,3 +362,77 @@ def render_multi(scenes: list, *, hdr64=True, tonemap: int = TONEMAP_NONE, stats
     if stats:
         out["trace_rays"], out["shadow_rays"] = st.trace_rays, st.shadow_rays
     return out
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId (rt_comm_unique_id): made on one rank, handed to all of them."""
+    buf = (ctypes.c_uint8 * RT_COMM_ID_BYTES)()
+    _check(load_library().rt_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """One rank of a row-tiled multi-GPU frame (rt_comm): render this rank's rows, one RCCL
+    gather to rank 0, assembled into rank 0's device framebuffers (rt_render_gather)."""
+
+    def __init__(self, ctx: Context, nranks: int, rank: int, uid: bytes, _handle=None):
+        L = load_library()
+        self.ctx = ctx
+        self.nranks, self.rank = nranks, rank
+        self._h = ctypes.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+            return
+        if len(uid) != RT_COMM_ID_BYTES:
+            raise ValueError("unique id must be RT_COMM_ID_BYTES bytes")
+        idbuf = (ctypes.c_uint8 * RT_COMM_ID_BYTES).from_buffer_copy(uid)
+        _check(L.rt_comm_create(ctx.handle, nranks, rank, idbuf, ctypes.byref(self._h)))
+
+    @classmethod
+    def create_all(cls, ctxs: list) -> list:
+        """n communicators over n distinct devices from this process (rt_comm_create_all)."""
+        n = len(ctxs)
+        hs = (ctypes.c_void_p * n)(*[c.handle for c in ctxs])
+        out = (ctypes.c_void_p * n)()
+        _check(load_library().rt_comm_create_all(hs, n, out))
+        return [cls(c, n, i, b"", _handle=ctypes.c_void_p(out[i])) for i, c in enumerate(ctxs)]
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            _lib.rt_comm_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def render_gather(self, dscene: "DeviceScene", opts: RenderOpts, outputs: int,
+                      d_hdr64: int | None = None, d_hdr32: int | None = None,
+                      d_ldr: int | None = None):
+        """Collective (every rank): enqueue this rank's rows + the gather (+ rank 0's
+        assembly into the d_* device framebuffers) on the context's stream."""
+        _check(_lib.rt_render_gather(self._h, dscene._h, dscene.camera.ctypes.data,
+                                     ctypes.byref(opts), outputs, d_hdr64, d_hdr32, d_ldr))
+
+    def timing(self, reset: bool = False) -> GatherTiming:
+        t = GatherTiming()
+        _check(_lib.rt_comm_timing(self._h, ctypes.byref(t), int(reset)))
+        return t
+
+
+def render_gather_all(comms: list, scenes: list, opts: RenderOpts, outputs: int,
+                      d_hdr64: int | None = None, d_hdr32: int | None = None,
+                      d_ldr: int | None = None):
+    """rt_render_gather_all: every rank of a Comm.create_all group from this process."""
+    n = len(comms)
+    cs = (ctypes.c_void_p * n)(*[c.handle for c in comms])
+    ss = (ctypes.c_void_p * n)(*[s._h for s in scenes])
+    _check(load_library().rt_render_gather_all(cs, ss, n, scenes[0].camera.ctypes.data,
+                                               ctypes.byref(opts), outputs, d_hdr64, d_hdr32,
+                                               d_ldr))

@@ -18,6 +18,7 @@
 #include <utility>
 #include <vector>
 
+#include "rt_context.hpp"
 #include "rt_internal.hpp"
 #include "rt_wavefront.hpp"
 
@@ -25,7 +26,7 @@
 
 using namespace rtamd;
 
-namespace {
+namespace rtamd {
 
 thread_local std::string g_last_error;
 
@@ -39,88 +40,9 @@ rt_status hip_fail(hipError_t e, const char* what) {
                 std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define RT_HIP(call)                                    \
-    do {                                                \
-        hipError_t e_ = (call);                         \
-        if (e_ != hipSuccess) return hip_fail(e_, #call); \
-    } while (0)
+}  // namespace rtamd
 
-struct DeviceBuffer {
-    void* ptr = nullptr;
-    size_t bytes = 0;
-    hipError_t ensure(size_t need) {
-        if (need <= bytes) return hipSuccess;
-        if (ptr) (void)hipFree(ptr);
-        ptr = nullptr;
-        bytes = 0;
-        hipError_t e = hipMalloc(&ptr, need);
-        if (e == hipSuccess) bytes = need;
-        return e;
-    }
-    void release() {
-        if (ptr) (void)hipFree(ptr);
-        ptr = nullptr;
-        bytes = 0;
-    }
-};
-
-// Restores the caller's current device on scope exit.
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
-
-}  // namespace
-
-struct rt_context {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipStream_t own_stream = nullptr;
-    size_t lds_limit = 0;
-    DeviceBuffer out64, out32, ldr, tm_in, tm_out, dbg, rays;
-    DeviceBuffer counters;  // 2 x u64
-    DeviceBuffer wf, wf_ctl;  // breadth-first TraceRay arena + its control block
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
-    double timed_ms = 0.0;
-    uint64_t launches = 0;
-};
-
-struct rt_scene {
-    rt_context* ctx = nullptr;
-    DeviceBuffer buf;
-    int32_t ns = 0, np = 0, nt = 0, nl = 0;
-    size_t off_sph = 0, off_sph_mat = 0, off_pl = 0, off_pl_mat = 0, off_tri = 0, off_tri_mat = 0,
-           off_lt = 0;
-    bool any_transparent = false;
-    double max_specular = 0.0;  // NaN-aware: stored as +inf when a NaN specular exists
-    bool has_area = false;
-    rt_area_light area{};
-    size_t off_bvh = 0, off_bvh_tri = 0;  // triangle BVH, when bvh_nodes > 0
-    int32_t bvh_nodes = 0;
-    // Packet-kernel LDS images, one per camera position this scene was rendered from more than
-    // once (the image depends on the spheres, planes, point lights and camera position only).  An
-    // entry is written once, by packet_image_kernel on the stream of the render that created
-    // it; renders on other streams wait for its event until it has completed.  Never rewritten
-    // or freed before the scene, so a launch in flight never sees it change.
-    struct PkImage {
-        double cam[3];
-        DeviceBuffer buf;
-        hipEvent_t ready = nullptr;
-        hipStream_t stream = nullptr;
-        bool done = false;
-    };
-    mutable std::vector<PkImage> pk_images;
-    mutable std::vector<std::array<double, 3>> pk_seen;  // cameras rendered once, no image yet
-};
-
-namespace {
+namespace rtamd {
 
 // Rows a render call produces: [row_begin, row_end), or with row_cycle > 1 the row_block-row
 // blocks starting at row_begin + k*row_cycle*row_block inside it (rt_render_opts).
@@ -321,8 +243,8 @@ rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
     return RT_OK;
 }
 
-rt_status enqueue(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
-                  const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr) {
+rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
+                         const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr) {
     TraceParams p;
     int path;
     bool lds;
@@ -412,7 +334,7 @@ rt_status enqueue(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
     return RT_OK;
 }
 
-}  // namespace
+}  // namespace rtamd
 
 extern "C" {
 
@@ -477,6 +399,7 @@ rt_status rt_context_destroy(rt_context* ctx) {
     for (DeviceBuffer* b : {&ctx->out64, &ctx->out32, &ctx->ldr, &ctx->tm_in, &ctx->tm_out,
                             &ctx->dbg, &ctx->rays, &ctx->counters, &ctx->wf, &ctx->wf_ctl})
         b->release();
+    release_group(ctx);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return RT_OK;
@@ -650,7 +573,7 @@ rt_status rt_render_device(rt_context* ctx, const rt_scene* sc, const rt_camera*
                            const rt_render_opts* opts, void* d64, void* d32, void* dldr) {
     if (!ctx) return fail(RT_ERR_INVALID_ARG, "context is NULL");
     DeviceGuard g(ctx->device);
-    return enqueue(ctx, sc, cam, opts, static_cast<double*>(d64), static_cast<float*>(d32),
+    return enqueue_render(ctx, sc, cam, opts, static_cast<double*>(d64), static_cast<float*>(d32),
                    static_cast<uint8_t*>(dldr));
 }
 
@@ -673,7 +596,7 @@ rt_status rt_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
     if (stats) {
         RT_HIP(hipMemsetAsync(ctx->counters.ptr, 0, 2 * sizeof(unsigned long long), ctx->stream));
     }
-    st = enqueue(ctx, sc, cam, &o, h64 ? static_cast<double*>(ctx->out64.ptr) : nullptr,
+    st = enqueue_render(ctx, sc, cam, &o, h64 ? static_cast<double*>(ctx->out64.ptr) : nullptr,
                  h32 ? static_cast<float*>(ctx->out32.ptr) : nullptr,
                  hldr ? static_cast<uint8_t*>(ctx->ldr.ptr) : nullptr);
     if (st != RT_OK) return st;
@@ -697,95 +620,6 @@ rt_status rt_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
             if (st != RT_OK) return st;
             stats->kernel_ms = ctx->timed_ms;
             stats->launches = ctx->launches;
-        }
-    }
-    return RT_OK;
-}
-
-rt_status rt_render_multi(rt_context* const* ctxs, rt_scene* const* scenes, int n,
-                          const rt_camera* cam, const rt_render_opts* opts, double* h64,
-                          float* h32, uint8_t* hldr, rt_stats* stats) {
-    if (n < 1 || !ctxs || !scenes) return fail(RT_ERR_INVALID_ARG, "rt_render_multi: n < 1 or NULL");
-    for (int i = 0; i < n; ++i) {
-        if (!ctxs[i] || !scenes[i] || scenes[i]->ctx != ctxs[i])
-            return fail(RT_ERR_INVALID_ARG, "rt_render_multi: scene " + std::to_string(i) +
-                                                " missing or not of context " + std::to_string(i));
-        for (int j = 0; j < i; ++j)
-            if (ctxs[j] == ctxs[i])  // each context renders into its own buffers
-                return fail(RT_ERR_INVALID_ARG, "rt_render_multi: context repeated");
-    }
-    rt_status st = validate_camera(cam);
-    if (st != RT_OK) return st;
-    rt_render_opts base;
-    if (opts) base = *opts;
-    else rt_render_opts_default(&base);
-    if (base.row_begin != 0 || (base.row_end != 0 && base.row_end != cam->height) ||
-        base.row_cycle > 1)
-        return fail(RT_ERR_INVALID_ARG, "rt_render_multi renders the whole image; the row "
-                                        "split is its own (row_block only)");
-    if (stats) base.flags |= RT_FLAG_COUNT_RAYS;
-    const uint32_t H = cam->height, W = cam->width;
-    const uint32_t block = n == 1 ? 0 : (base.row_block ? base.row_block : 16);
-    std::vector<rt_render_opts> o(static_cast<size_t>(n), base);
-    std::vector<uint32_t> rows(static_cast<size_t>(n));
-    // 1. every context renders its rows (block-cyclic) into its own device buffers, async
-    for (int i = 0; i < n; ++i) {
-        rt_context* ctx = ctxs[i];
-        DeviceGuard g(ctx->device);
-        o[i].row_end = H;
-        if (block) {
-            o[i].row_begin = static_cast<uint32_t>(i) * block;
-            o[i].row_block = static_cast<uint16_t>(block);
-            o[i].row_cycle = static_cast<uint16_t>(n);
-            if (o[i].row_begin >= H) {
-                rows[i] = 0;
-                continue;
-            }
-        }
-        rows[i] = rendered_rows(o[i], H);
-        const size_t npx = static_cast<size_t>(rows[i]) * W;
-        if (h64) RT_HIP(ctx->out64.ensure(npx * 3 * sizeof(double)));
-        if (h32) RT_HIP(ctx->out32.ensure(npx * 3 * sizeof(float)));
-        if (hldr) RT_HIP(ctx->ldr.ensure(npx * 3));
-        if (stats)
-            RT_HIP(hipMemsetAsync(ctx->counters.ptr, 0, 2 * sizeof(unsigned long long),
-                                  ctx->stream));
-        st = enqueue(ctx, scenes[i], cam, &o[i],
-                     h64 ? static_cast<double*>(ctx->out64.ptr) : nullptr,
-                     h32 ? static_cast<float*>(ctx->out32.ptr) : nullptr,
-                     hldr ? static_cast<uint8_t*>(ctx->ldr.ptr) : nullptr);
-        if (st != RT_OK) return st;
-    }
-    // 2. gather: each context's packed rows back to their image rows in the caller's buffers
-    if (stats) std::memset(stats, 0, sizeof *stats);
-    for (int i = 0; i < n; ++i) {
-        if (rows[i] == 0) continue;
-        rt_context* ctx = ctxs[i];
-        DeviceGuard g(ctx->device);
-        const size_t row64 = size_t(W) * 3 * sizeof(double), row32 = size_t(W) * 3 * sizeof(float),
-                     row8 = size_t(W) * 3;
-        uint32_t k = 0;  // packed row of this context
-        for (uint32_t b0 = o[i].row_begin; b0 < H; b0 += block ? block * n : H) {
-            const uint32_t nb = block ? std::min(block, H - b0) : rows[i];
-            if (h64)
-                RT_HIP(hipMemcpyAsync(reinterpret_cast<char*>(h64) + b0 * row64,
-                                      static_cast<char*>(ctx->out64.ptr) + k * row64, nb * row64,
-                                      hipMemcpyDeviceToHost, ctx->stream));
-            if (h32)
-                RT_HIP(hipMemcpyAsync(reinterpret_cast<char*>(h32) + b0 * row32,
-                                      static_cast<char*>(ctx->out32.ptr) + k * row32, nb * row32,
-                                      hipMemcpyDeviceToHost, ctx->stream));
-            if (hldr)
-                RT_HIP(hipMemcpyAsync(hldr + b0 * row8, static_cast<char*>(ctx->ldr.ptr) + k * row8,
-                                      nb * row8, hipMemcpyDeviceToHost, ctx->stream));
-            k += nb;
-        }
-        RT_HIP(hipStreamSynchronize(ctx->stream));
-        if (stats) {
-            unsigned long long c[2] = {0, 0};
-            RT_HIP(hipMemcpy(c, ctx->counters.ptr, sizeof c, hipMemcpyDeviceToHost));
-            stats->trace_rays += c[0];
-            stats->shadow_rays += c[1];
         }
     }
     return RT_OK;

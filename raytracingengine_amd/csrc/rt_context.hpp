@@ -1,0 +1,123 @@
+// rt_context.hpp — the C-ABI objects (rt_context, rt_scene) and the helpers the C-ABI
+// translation units share (rt_capi.cpp: single device; rt_multi.cpp: RCCL multi-GPU frames).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "rt_capi.h"
+#include "rt_internal.hpp"
+
+namespace rtamd {
+
+// Sets the calling thread's rt_last_error() message and returns st.
+rt_status fail(rt_status st, const std::string& msg);
+rt_status hip_fail(hipError_t e, const char* what);
+
+#define RT_HIP(call)                                    \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return rtamd::hip_fail(e_, #call); \
+    } while (0)
+
+struct DeviceBuffer {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&ptr, need);
+        if (e == hipSuccess) bytes = need;
+        return e;
+    }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+};
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace rtamd
+
+struct rt_comm;
+
+struct rt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    size_t lds_limit = 0;
+    rtamd::DeviceBuffer out64, out32, ldr, tm_in, tm_out, dbg, rays;
+    rtamd::DeviceBuffer counters;  // 2 x u64
+    rtamd::DeviceBuffer wf, wf_ctl;  // breadth-first TraceRay arena + its control block
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
+    double timed_ms = 0.0;
+    uint64_t launches = 0;
+    // rt_render_multi: RCCL communicators over the devices of the last context list this
+    // context led (rt_multi.cpp); destroyed with the context
+    std::vector<rt_context*> group_ctxs;
+    std::vector<rt_comm*> group_comms;
+};
+
+struct rt_scene {
+    rt_context* ctx = nullptr;
+    rtamd::DeviceBuffer buf;
+    int32_t ns = 0, np = 0, nt = 0, nl = 0;
+    size_t off_sph = 0, off_sph_mat = 0, off_pl = 0, off_pl_mat = 0, off_tri = 0, off_tri_mat = 0,
+           off_lt = 0;
+    bool any_transparent = false;
+    double max_specular = 0.0;  // NaN-aware: stored as +inf when a NaN specular exists
+    bool has_area = false;
+    rt_area_light area{};
+    size_t off_bvh = 0, off_bvh_tri = 0;  // triangle BVH, when bvh_nodes > 0
+    int32_t bvh_nodes = 0;
+    // Packet-kernel LDS images, one per camera position this scene was rendered from more than
+    // once (the image depends on the spheres, planes, point lights and camera position only).  An
+    // entry is written once, by packet_image_kernel on the stream of the render that created
+    // it; renders on other streams wait for its event until it has completed.  Never rewritten
+    // or freed before the scene, so a launch in flight never sees it change.
+    struct PkImage {
+        double cam[3];
+        rtamd::DeviceBuffer buf;
+        hipEvent_t ready = nullptr;
+        hipStream_t stream = nullptr;
+        bool done = false;
+    };
+    mutable std::vector<PkImage> pk_images;
+    mutable std::vector<std::array<double, 3>> pk_seen;  // cameras rendered once, no image yet
+};
+
+namespace rtamd {
+
+// Rows a render call produces: [row_begin, row_end), or with row_cycle > 1 the row_block-row
+// blocks starting at row_begin + k*row_cycle*row_block inside it (rt_render_opts).
+uint32_t rendered_rows(const rt_render_opts& o, uint32_t height);
+rt_status validate_camera(const rt_camera* cam);
+// Enqueues one render (plus the counting pass with RT_FLAG_COUNT_RAYS) on ctx's stream into
+// device outputs in the packed row order of opts.  The caller holds a DeviceGuard.
+rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
+                         const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr);
+// Adds the elapsed time of completed RT_FLAG_TIME_KERNEL event pairs to the context totals.
+rt_status harvest_events(rt_context* ctx, bool all);
+// rt_multi.cpp: releases the communicators rt_render_multi cached in ctx.
+void release_group(rt_context* ctx);
+
+}  // namespace rtamd

@@ -1,0 +1,616 @@
+// rt_multi.cpp — Scene::RenderImage over the GPUs of a node (RE/Scene.h:318-325):
+// the frame's rows are split block-cyclically over the ranks, every rank renders its rows, ONE
+// RCCL gather per output moves them to rank 0 over xGMI, and rank 0 writes them into image
+// order (rt_assemble.hip).  Two ways in:
+//   * one process per GPU: rt_comm_create (ncclCommInitRank) + rt_render_gather on every rank;
+//   * one process driving every GPU (the reference's single-process RenderImage):
+//     rt_comm_create_all (ncclCommInitAll) + rt_render_gather_all, and rt_render_multi on top of
+//     it for host framebuffers (the drop-in Scene::SetDevices path).
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rt_capi.h"
+#include "rt_context.hpp"
+#include "rt_internal.hpp"
+
+using namespace rtamd;
+
+namespace rtamd {
+hipError_t launch_assemble_rows(const void* gathered, void* image, size_t row_bytes,
+                                uint32_t height, uint32_t block, uint32_t n, uint32_t max_rows,
+                                hipStream_t stream);
+}
+
+static_assert(RT_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "rt_capi.h id size");
+
+struct rt_comm {
+    rt_context* ctx = nullptr;  // the context whose device and stream the collectives use
+    int device = -1;
+    ncclComm_t nccl = nullptr;
+    int nranks = 1, rank = 0;
+    // per output kind (RT_OUT_HDR64, _HDR32, _LDR): this rank's packed rows (send), and on
+    // rank 0 the n gathered buffers (recv)
+    DeviceBuffer send[3], recv[3];
+    // RT_FLAG_TIME_KERNEL frames: events before the render, after it, after the gather and
+    // after the assembly
+    struct Ev { hipEvent_t e[4]; };
+    std::vector<Ev> pending, spare;
+    double render_ms = 0, gather_ms = 0, assemble_ms = 0;
+    uint64_t frames = 0;
+    uint32_t rows = 0, max_rows = 0;
+};
+
+namespace {
+
+constexpr int kOutputs[3] = {RT_OUT_HDR64, RT_OUT_HDR32, RT_OUT_LDR};
+constexpr uint32_t kDefaultBlock = 16;
+
+size_t bytes_per_px(int k) { return k == 0 ? 24 : (k == 1 ? 12 : 3); }
+
+rt_status nccl_fail(ncclResult_t r, const char* what) {
+    return fail(RT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+#define RT_NCCL(call)                                       \
+    do {                                                    \
+        ncclResult_t r_ = (call);                           \
+        if (r_ != ncclSuccess) return nccl_fail(r_, #call); \
+    } while (0)
+
+// This rank's share of the frame: rt_render_opts selecting the block-cyclic row set `rank` of
+// `n` (a contiguous full frame when n == 1), and the rows it produces.
+struct Plan {
+    rt_render_opts opts;
+    uint32_t block = 0, rows = 0, max_rows = 0;
+};
+
+rt_status make_plan(const rt_camera* cam, const rt_render_opts* in, int n, int rank, Plan& pl) {
+    rt_render_opts o;
+    if (in) o = *in;
+    else rt_render_opts_default(&o);
+    if (o.row_begin != 0 || (o.row_end != 0 && o.row_end != cam->height) || o.row_cycle > 1)
+        return fail(RT_ERR_INVALID_ARG, "multi-GPU frames render the whole image; the row "
+                                        "split is their own (set row_block only)");
+    const uint32_t H = cam->height;
+    pl.block = n == 1 ? H : (o.row_block ? o.row_block : kDefaultBlock);
+    o.row_end = H;
+    o.row_begin = static_cast<uint32_t>(rank) * pl.block;
+    o.row_block = n == 1 ? 0 : static_cast<uint16_t>(pl.block);
+    o.row_cycle = n == 1 ? 0 : static_cast<uint16_t>(n);
+    pl.opts = o;
+    pl.rows = o.row_begin < H ? rendered_rows(o, H) : 0;
+    pl.max_rows = 0;
+    for (int r = 0; r < n; ++r) {
+        rt_render_opts q = o;
+        q.row_begin = static_cast<uint32_t>(r) * pl.block;
+        if (q.row_begin < H) pl.max_rows = std::max(pl.max_rows, rendered_rows(q, H));
+    }
+    return RT_OK;
+}
+
+rt_status check_outputs(int outputs) {
+    if (outputs == 0 || (outputs & ~(RT_OUT_HDR64 | RT_OUT_HDR32 | RT_OUT_LDR)))
+        return fail(RT_ERR_INVALID_ARG, "outputs must be a non-empty set of RT_OUT_* bits");
+    return RT_OK;
+}
+
+rt_status harvest(rt_comm* c, bool all) {
+    size_t done = 0;
+    for (auto& ev : c->pending) {
+        if (!all && hipEventQuery(ev.e[3]) != hipSuccess) break;
+        RT_HIP(hipEventSynchronize(ev.e[3]));
+        float a = 0, b = 0, d = 0;
+        RT_HIP(hipEventElapsedTime(&a, ev.e[0], ev.e[1]));
+        RT_HIP(hipEventElapsedTime(&b, ev.e[1], ev.e[2]));
+        RT_HIP(hipEventElapsedTime(&d, ev.e[2], ev.e[3]));
+        c->render_ms += a;
+        c->gather_ms += b;
+        c->assemble_ms += d;
+        c->frames += 1;
+        c->spare.push_back(ev);
+        ++done;
+    }
+    c->pending.erase(c->pending.begin(), c->pending.begin() + static_cast<long>(done));
+    return RT_OK;
+}
+
+rt_status record(rt_comm* c, rt_comm::Ev* ev, int k) {
+    if (!ev) return RT_OK;
+    RT_HIP(hipEventRecord(ev->e[k], c->ctx->stream));
+    return RT_OK;
+}
+
+// Phase 1 of a frame on one rank: this rank's rows rendered into its send buffers.
+rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
+                      const rt_render_opts* opts, int outputs, Plan& pl, rt_comm::Ev*& ev) {
+    rt_context* ctx = c->ctx;
+    if (sc->ctx != ctx)
+        return fail(RT_ERR_INVALID_ARG, "scene does not belong to the communicator's context");
+    rt_status st = make_plan(cam, opts, c->nranks, c->rank, pl);
+    if (st != RT_OK) return st;
+    const size_t npx = static_cast<size_t>(pl.max_rows) * cam->width;
+    for (int k = 0; k < 3; ++k) {
+        if (!(outputs & kOutputs[k])) continue;
+        RT_HIP(c->send[k].ensure(npx * bytes_per_px(k)));
+        if (c->rank == 0) RT_HIP(c->recv[k].ensure(npx * bytes_per_px(k) * c->nranks));
+    }
+    c->rows = pl.rows;
+    c->max_rows = pl.max_rows;
+    ev = nullptr;
+    if (pl.opts.flags & RT_FLAG_TIME_KERNEL) {
+        if (c->pending.size() >= 256) {
+            st = harvest(c, false);
+            if (st != RT_OK) return st;
+        }
+        c->pending.emplace_back();
+        rt_comm::Ev& e = c->pending.back();
+        if (!c->spare.empty()) {
+            e = c->spare.back();
+            c->spare.pop_back();
+        } else {
+            for (auto& x : e.e) RT_HIP(hipEventCreate(&x));
+        }
+        ev = &e;
+    }
+    // the frame's own events replace the per-launch ones of the render
+    pl.opts.flags &= ~RT_FLAG_TIME_KERNEL;
+    if (!(outputs & RT_OUT_LDR)) pl.opts.tonemap = RT_TONEMAP_NONE;
+    else if (pl.opts.tonemap == RT_TONEMAP_NONE)
+        return fail(RT_ERR_INVALID_ARG, "RT_OUT_LDR needs opts->tonemap");
+    st = record(c, ev, 0);
+    if (st != RT_OK) return st;
+    if (pl.rows > 0) {
+        st = enqueue_render(ctx, sc, cam, &pl.opts,
+                            (outputs & RT_OUT_HDR64) ? static_cast<double*>(c->send[0].ptr) : nullptr,
+                            (outputs & RT_OUT_HDR32) ? static_cast<float*>(c->send[1].ptr) : nullptr,
+                            (outputs & RT_OUT_LDR) ? static_cast<uint8_t*>(c->send[2].ptr) : nullptr);
+        if (st != RT_OK) return st;
+    }
+    return record(c, ev, 1);
+}
+
+// Phase 2: one ncclGather per output (inside the caller's group when several are issued).
+rt_status gather_part(rt_comm* c, const rt_camera* cam, int outputs, const Plan& pl) {
+    const size_t npx = static_cast<size_t>(pl.max_rows) * cam->width;
+    for (int k = 0; k < 3; ++k) {
+        if (!(outputs & kOutputs[k])) continue;
+        void* recv = c->rank == 0 ? c->recv[k].ptr : c->send[k].ptr;
+        RT_NCCL(ncclGather(c->send[k].ptr, recv, npx * bytes_per_px(k), ncclUint8, 0, c->nccl,
+                           c->ctx->stream));
+    }
+    return RT_OK;
+}
+
+// Phase 3 (rank 0): gathered rows into image order in the caller's device framebuffers.
+rt_status assemble_part(rt_comm* c, const rt_camera* cam, int outputs, const Plan& pl,
+                        void* const* dst, rt_comm::Ev* ev) {
+    rt_status st = record(c, ev, 2);
+    if (st != RT_OK) return st;
+    if (c->rank == 0) {
+        for (int k = 0; k < 3; ++k) {
+            if (!(outputs & kOutputs[k]) || !dst[k]) continue;
+            RT_HIP(launch_assemble_rows(c->recv[k].ptr, dst[k], size_t(cam->width) * bytes_per_px(k),
+                                        cam->height, pl.block, static_cast<uint32_t>(c->nranks),
+                                        pl.max_rows, c->ctx->stream));
+        }
+    }
+    return record(c, ev, 3);
+}
+
+rt_status check_root_outputs(const rt_comm* c, int outputs, void* const* dst) {
+    if (c->rank != 0) return RT_OK;
+    for (int k = 0; k < 3; ++k)
+        if ((outputs & kOutputs[k]) && !dst[k])
+            return fail(RT_ERR_INVALID_ARG, "rank 0 needs a device framebuffer for every "
+                                            "requested output");
+    return RT_OK;
+}
+
+// Contexts that share a GPU (RCCL allows one rank per GPU): the same block-cyclic split, each
+// context's rows copied straight into the caller's host rows (every device's copies are
+// enqueued before the first synchronisation, so the devices' transfers overlap).
+rt_status render_multi_host(rt_context* const* ctxs, rt_scene* const* scenes, int n,
+                            const rt_camera* cam, const rt_render_opts* opts, double* h64,
+                            float* h32, uint8_t* hldr, rt_stats* stats) {
+    // (arguments validated by rt_render_multi)
+    rt_status st = RT_OK;
+    rt_render_opts base;
+    if (opts) base = *opts;
+    else rt_render_opts_default(&base);
+    if (base.row_begin != 0 || (base.row_end != 0 && base.row_end != cam->height) ||
+        base.row_cycle > 1)
+        return fail(RT_ERR_INVALID_ARG, "rt_render_multi renders the whole image; the row "
+                                        "split is its own (row_block only)");
+    if (stats) base.flags |= RT_FLAG_COUNT_RAYS;
+    const uint32_t H = cam->height, W = cam->width;
+    const uint32_t block = n == 1 ? 0 : (base.row_block ? base.row_block : 16);
+    std::vector<rt_render_opts> o(static_cast<size_t>(n), base);
+    std::vector<uint32_t> rows(static_cast<size_t>(n));
+    // 1. every context renders its rows (block-cyclic) into its own device buffers, async
+    for (int i = 0; i < n; ++i) {
+        rt_context* ctx = ctxs[i];
+        DeviceGuard g(ctx->device);
+        o[i].row_end = H;
+        if (block) {
+            o[i].row_begin = static_cast<uint32_t>(i) * block;
+            o[i].row_block = static_cast<uint16_t>(block);
+            o[i].row_cycle = static_cast<uint16_t>(n);
+            if (o[i].row_begin >= H) {
+                rows[i] = 0;
+                continue;
+            }
+        }
+        rows[i] = rendered_rows(o[i], H);
+        const size_t npx = static_cast<size_t>(rows[i]) * W;
+        if (h64) RT_HIP(ctx->out64.ensure(npx * 3 * sizeof(double)));
+        if (h32) RT_HIP(ctx->out32.ensure(npx * 3 * sizeof(float)));
+        if (hldr) RT_HIP(ctx->ldr.ensure(npx * 3));
+        if (stats)
+            RT_HIP(hipMemsetAsync(ctx->counters.ptr, 0, 2 * sizeof(unsigned long long),
+                                  ctx->stream));
+        st = enqueue_render(ctx, scenes[i], cam, &o[i],
+                     h64 ? static_cast<double*>(ctx->out64.ptr) : nullptr,
+                     h32 ? static_cast<float*>(ctx->out32.ptr) : nullptr,
+                     hldr ? static_cast<uint8_t*>(ctx->ldr.ptr) : nullptr);
+        if (st != RT_OK) return st;
+    }
+    // 2. gather: each context's packed rows back to their image rows in the caller's buffers
+    if (stats) std::memset(stats, 0, sizeof *stats);
+    for (int i = 0; i < n; ++i) {
+        if (rows[i] == 0) continue;
+        rt_context* ctx = ctxs[i];
+        DeviceGuard g(ctx->device);
+        const size_t row64 = size_t(W) * 3 * sizeof(double), row32 = size_t(W) * 3 * sizeof(float),
+                     row8 = size_t(W) * 3;
+        uint32_t k = 0;  // packed row of this context
+        for (uint32_t b0 = o[i].row_begin; b0 < H; b0 += block ? block * n : H) {
+            const uint32_t nb = block ? std::min(block, H - b0) : rows[i];
+            if (h64)
+                RT_HIP(hipMemcpyAsync(reinterpret_cast<char*>(h64) + b0 * row64,
+                                      static_cast<char*>(ctx->out64.ptr) + k * row64, nb * row64,
+                                      hipMemcpyDeviceToHost, ctx->stream));
+            if (h32)
+                RT_HIP(hipMemcpyAsync(reinterpret_cast<char*>(h32) + b0 * row32,
+                                      static_cast<char*>(ctx->out32.ptr) + k * row32, nb * row32,
+                                      hipMemcpyDeviceToHost, ctx->stream));
+            if (hldr)
+                RT_HIP(hipMemcpyAsync(hldr + b0 * row8, static_cast<char*>(ctx->ldr.ptr) + k * row8,
+                                      nb * row8, hipMemcpyDeviceToHost, ctx->stream));
+            k += nb;
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        rt_context* ctx = ctxs[i];
+        DeviceGuard g(ctx->device);
+        RT_HIP(hipStreamSynchronize(ctx->stream));
+        if (o[i].flags & RT_FLAG_TIME_KERNEL) {
+            st = harvest_events(ctx, true);
+            if (st != RT_OK) return st;
+        }
+        if (rows[i] == 0 || !stats) continue;
+        {
+            unsigned long long c[2] = {0, 0};
+            RT_HIP(hipMemcpy(c, ctx->counters.ptr, sizeof c, hipMemcpyDeviceToHost));
+            stats->trace_rays += c[0];
+            stats->shadow_rays += c[1];
+            stats->kernel_ms += ctx->timed_ms;
+            stats->launches += ctx->launches;
+        }
+    }
+    return RT_OK;
+}
+
+// One frame over n contexts into host framebuffers (rt_capi.h rt_render_multi).  Distinct GPUs:
+// the RCCL path — communicators over the contexts' devices (ncclCommInitAll, cached in ctxs[0]
+// until the context list changes), rt_render_gather_all into ctxs[0]'s device framebuffers,
+// one device-to-host copy per output from rank 0.
+rt_status render_multi_rccl(rt_context* const* ctxs, rt_scene* const* scenes, int n,
+                            const rt_camera* cam, const rt_render_opts* opts, int outputs,
+                            double* h64, float* h32, uint8_t* hldr, rt_stats* stats) {
+    rt_context* root = ctxs[0];
+    bool same = root->group_ctxs.size() == static_cast<size_t>(n);
+    for (int i = 0; same && i < n; ++i)
+        same = root->group_ctxs[i] == ctxs[i] && root->group_comms[i]->device == ctxs[i]->device;
+    if (!same) {
+        release_group(root);
+        std::vector<rt_comm*> comms(static_cast<size_t>(n), nullptr);
+        rt_status st = rt_comm_create_all(ctxs, n, comms.data());
+        if (st != RT_OK) return st;
+        root->group_ctxs.assign(ctxs, ctxs + n);
+        root->group_comms = comms;
+    }
+    for (int i = 0; i < n; ++i) root->group_comms[i]->ctx = ctxs[i];
+    rt_render_opts o;
+    if (opts) o = *opts;
+    else rt_render_opts_default(&o);
+    if (stats) o.flags |= RT_FLAG_COUNT_RAYS;
+    if (stats)
+        for (int i = 0; i < n; ++i) {
+            DeviceGuard g(ctxs[i]->device);
+            RT_HIP(hipMemsetAsync(ctxs[i]->counters.ptr, 0, 2 * sizeof(unsigned long long),
+                                  ctxs[i]->stream));
+        }
+    const size_t npx = static_cast<size_t>(cam->width) * cam->height;
+    {
+        DeviceGuard g(root->device);
+        if (h64) RT_HIP(root->out64.ensure(npx * 3 * sizeof(double)));
+        if (h32) RT_HIP(root->out32.ensure(npx * 3 * sizeof(float)));
+        if (hldr) RT_HIP(root->ldr.ensure(npx * 3));
+    }
+    rt_status st = rt_render_gather_all(root->group_comms.data(), scenes, n, cam, &o, outputs,
+                                        h64 ? root->out64.ptr : nullptr,
+                                        h32 ? root->out32.ptr : nullptr,
+                                        hldr ? root->ldr.ptr : nullptr);
+    if (st != RT_OK) return st;
+    {
+        DeviceGuard g(root->device);
+        if (h64)
+            RT_HIP(hipMemcpyAsync(h64, root->out64.ptr, npx * 3 * sizeof(double),
+                                  hipMemcpyDeviceToHost, root->stream));
+        if (h32)
+            RT_HIP(hipMemcpyAsync(h32, root->out32.ptr, npx * 3 * sizeof(float),
+                                  hipMemcpyDeviceToHost, root->stream));
+        if (hldr)
+            RT_HIP(hipMemcpyAsync(hldr, root->ldr.ptr, npx * 3, hipMemcpyDeviceToHost,
+                                  root->stream));
+    }
+    if (stats) std::memset(stats, 0, sizeof *stats);
+    for (int i = 0; i < n; ++i) {
+        DeviceGuard g(ctxs[i]->device);
+        RT_HIP(hipStreamSynchronize(ctxs[i]->stream));
+        if (!stats) continue;
+        unsigned long long c[2] = {0, 0};
+        RT_HIP(hipMemcpy(c, ctxs[i]->counters.ptr, sizeof c, hipMemcpyDeviceToHost));
+        stats->trace_rays += c[0];
+        stats->shadow_rays += c[1];
+    }
+    if (stats && (o.flags & RT_FLAG_TIME_KERNEL)) {  // the frame's render time on the slowest GPU
+        for (int i = 0; i < n; ++i) {
+            rt_gather_timing t;
+            st = rt_comm_timing(root->group_comms[i], &t, 1);
+            if (st != RT_OK) return st;
+            stats->kernel_ms = std::max(stats->kernel_ms, t.render_ms);
+        }
+        stats->launches = 1;
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+rt_status rt_render_multi(rt_context* const* ctxs, rt_scene* const* scenes, int n,
+                          const rt_camera* cam, const rt_render_opts* opts, double* h64,
+                          float* h32, uint8_t* hldr, rt_stats* stats) {
+    if (n < 1 || !ctxs || !scenes) return fail(RT_ERR_INVALID_ARG, "rt_render_multi: n < 1 or NULL");
+    bool distinct = true;
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i] || !scenes[i] || scenes[i]->ctx != ctxs[i])
+            return fail(RT_ERR_INVALID_ARG, "rt_render_multi: scene " + std::to_string(i) +
+                                                " missing or not of context " + std::to_string(i));
+        for (int j = 0; j < i; ++j) {
+            if (ctxs[j] == ctxs[i])  // each context renders into its own buffers
+                return fail(RT_ERR_INVALID_ARG, "rt_render_multi: context repeated");
+            if (ctxs[j]->device == ctxs[i]->device) distinct = false;
+        }
+    }
+    rt_status st = validate_camera(cam);
+    if (st != RT_OK) return st;
+    const int outputs = (h64 ? RT_OUT_HDR64 : 0) | (h32 ? RT_OUT_HDR32 : 0) |
+                        (hldr ? RT_OUT_LDR : 0);
+    const char* env = std::getenv("RTAMD_MULTI_HOST");  // force the host assembly (tests)
+    if (distinct && outputs && !(env && std::atoi(env) == 1)) {
+        rt_render_opts o;
+        if (opts) o = *opts;
+        else rt_render_opts_default(&o);
+        if (!hldr) o.tonemap = RT_TONEMAP_NONE;
+        return render_multi_rccl(ctxs, scenes, n, cam, &o, outputs, h64, h32, hldr, stats);
+    }
+    return render_multi_host(ctxs, scenes, n, cam, opts, h64, h32, hldr, stats);
+}
+
+}  // extern "C"
+
+namespace rtamd {
+
+void release_group(rt_context* ctx) {
+    for (rt_comm* c : ctx->group_comms) rt_comm_destroy(c);
+    ctx->group_comms.clear();
+    ctx->group_ctxs.clear();
+}
+
+}  // namespace rtamd
+
+extern "C" {
+
+rt_status rt_comm_unique_id(uint8_t* id) {
+    if (!id) return fail(RT_ERR_INVALID_ARG, "id is NULL");
+    ncclUniqueId u;
+    RT_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, u.internal, sizeof u.internal);
+    return RT_OK;
+}
+
+rt_status rt_comm_create(rt_context* ctx, int nranks, int rank, const uint8_t* id,
+                         rt_comm** out) {
+    if (!ctx || !id || !out) return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_comm_create");
+    if (nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(RT_ERR_INVALID_ARG, "rank must be in [0, nranks)");
+    *out = nullptr;
+    DeviceGuard g(ctx->device);
+    rt_comm* c = new (std::nothrow) rt_comm();
+    if (!c) return fail(RT_ERR_OOM, "host allocation failed");
+    c->ctx = ctx;
+    c->device = ctx->device;
+    c->nranks = nranks;
+    c->rank = rank;
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, sizeof u.internal);
+    const ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return nccl_fail(r, "ncclCommInitRank");
+    }
+    *out = c;
+    return RT_OK;
+}
+
+rt_status rt_comm_create_all(rt_context* const* ctxs, int n, rt_comm** out) {
+    if (!ctxs || !out || n < 1) return fail(RT_ERR_INVALID_ARG, "rt_comm_create_all: n < 1 or NULL");
+    std::vector<int> devs(static_cast<size_t>(n));
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i]) return fail(RT_ERR_INVALID_ARG, "rt_comm_create_all: NULL context");
+        devs[i] = ctxs[i]->device;
+        for (int j = 0; j < i; ++j)
+            if (devs[j] == devs[i])  // RCCL: one rank per GPU
+                return fail(RT_ERR_INVALID_ARG, "rt_comm_create_all: device " +
+                                                    std::to_string(devs[i]) + " repeated");
+    }
+    std::vector<ncclComm_t> comms(static_cast<size_t>(n), nullptr);
+    {
+        DeviceGuard g(devs[0]);
+        RT_NCCL(ncclCommInitAll(comms.data(), n, devs.data()));
+    }
+    for (int i = 0; i < n; ++i) {
+        rt_comm* c = new (std::nothrow) rt_comm();
+        if (!c) {
+            for (int j = 0; j < i; ++j) rt_comm_destroy(out[j]);
+            for (int j = i; j < n; ++j) (void)ncclCommDestroy(comms[j]);
+            return fail(RT_ERR_OOM, "host allocation failed");
+        }
+        c->ctx = ctxs[i];
+        c->device = devs[i];
+        c->nccl = comms[i];
+        c->nranks = n;
+        c->rank = i;
+        out[i] = c;
+    }
+    return RT_OK;
+}
+
+rt_status rt_comm_destroy(rt_comm* c) {
+    if (!c) return RT_OK;
+    DeviceGuard g(c->device);
+    if (c->ctx && c->ctx->stream) (void)hipStreamSynchronize(c->ctx->stream);
+    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    for (auto* v : {&c->pending, &c->spare})
+        for (auto& ev : *v)
+            for (auto& x : ev.e) (void)hipEventDestroy(x);
+    for (int k = 0; k < 3; ++k) {
+        c->send[k].release();
+        c->recv[k].release();
+    }
+    delete c;
+    return RT_OK;
+}
+
+rt_status rt_render_gather(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
+                           const rt_render_opts* opts, int outputs, void* d_hdr64,
+                           void* d_hdr32, void* d_ldr) {
+    if (!c || !sc) return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_render_gather");
+    rt_status st = validate_camera(cam);
+    if (st == RT_OK) st = check_outputs(outputs);
+    void* const dst[3] = {d_hdr64, d_hdr32, d_ldr};
+    if (st == RT_OK) st = check_root_outputs(c, outputs, dst);
+    if (st != RT_OK) return st;
+    DeviceGuard g(c->device);
+    Plan pl;
+    rt_comm::Ev* ev = nullptr;
+    st = render_part(c, sc, cam, opts, outputs, pl, ev);
+    if (st != RT_OK) return st;
+    RT_NCCL(ncclGroupStart());
+    st = gather_part(c, cam, outputs, pl);
+    RT_NCCL(ncclGroupEnd());
+    if (st != RT_OK) return st;
+    return assemble_part(c, cam, outputs, pl, dst, ev);
+}
+
+rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, int n,
+                               const rt_camera* cam, const rt_render_opts* opts, int outputs,
+                               void* d_hdr64, void* d_hdr32, void* d_ldr) {
+    if (!comms || !scenes || n < 1) return fail(RT_ERR_INVALID_ARG, "rt_render_gather_all: n < 1 or NULL");
+    rt_status st = validate_camera(cam);
+    if (st == RT_OK) st = check_outputs(outputs);
+    if (st != RT_OK) return st;
+    for (int i = 0; i < n; ++i)
+        if (!comms[i] || !scenes[i] || comms[i]->nranks != n || comms[i]->rank != i)
+            return fail(RT_ERR_INVALID_ARG, "rt_render_gather_all: comms must be the n ranks of "
+                                            "one rt_comm_create_all, in rank order");
+    void* const dst[3] = {d_hdr64, d_hdr32, d_ldr};
+    st = check_root_outputs(comms[0], outputs, dst);
+    if (st != RT_OK) return st;
+    std::vector<Plan> pl(static_cast<size_t>(n));
+    std::vector<rt_comm::Ev*> ev(static_cast<size_t>(n), nullptr);
+    for (int i = 0; i < n; ++i) {  // 1. every GPU renders its rows (asynchronous)
+        DeviceGuard g(comms[i]->device);
+        st = render_part(comms[i], scenes[i], cam, opts, outputs, pl[i], ev[i]);
+        if (st != RT_OK) return st;
+    }
+    RT_NCCL(ncclGroupStart());  // 2. one gather per output over all GPUs
+    for (int i = 0; i < n && st == RT_OK; ++i) {
+        DeviceGuard g(comms[i]->device);
+        st = gather_part(comms[i], cam, outputs, pl[i]);
+    }
+    RT_NCCL(ncclGroupEnd());
+    if (st != RT_OK) return st;
+    for (int i = 0; i < n; ++i) {  // 3. rank 0 assembles; the others close their events
+        DeviceGuard g(comms[i]->device);
+        st = assemble_part(comms[i], cam, outputs, pl[i], dst, ev[i]);
+        if (st != RT_OK) return st;
+    }
+    return RT_OK;
+}
+
+rt_status rt_comm_timing(rt_comm* c, rt_gather_timing* out, int reset) {
+    if (!c) return fail(RT_ERR_INVALID_ARG, "comm is NULL");
+    DeviceGuard g(c->device);
+    rt_status st = harvest(c, true);
+    if (st != RT_OK) return st;
+    if (out) {
+        out->render_ms = c->render_ms;
+        out->gather_ms = c->gather_ms;
+        out->assemble_ms = c->assemble_ms;
+        out->frames = c->frames;
+        out->rows = c->rows;
+        out->max_rows = c->max_rows;
+    }
+    if (reset) {
+        c->render_ms = c->gather_ms = c->assemble_ms = 0;
+        c->frames = 0;
+    }
+    return RT_OK;
+}
+
+rt_status rt_debug_assemble_rows(rt_context* ctx, const void* gathered, size_t row_bytes,
+                                 uint32_t height, uint32_t block, uint32_t n, uint32_t max_rows,
+                                 void* image) {
+    if (!ctx || !gathered || !image || n < 1 || block < 1)
+        return fail(RT_ERR_INVALID_ARG, "bad argument to rt_debug_assemble_rows");
+    DeviceGuard g(ctx->device);
+    const size_t in_bytes = size_t(n) * max_rows * row_bytes, out_bytes = size_t(height) * row_bytes;
+    RT_HIP(ctx->dbg.ensure(in_bytes + out_bytes + 16));
+    char* d_in = static_cast<char*>(ctx->dbg.ptr);
+    // the image at an offset that keeps the 16-B path when row_bytes allows it
+    char* d_out = d_in + ((in_bytes + 15) & ~size_t(15));
+    RT_HIP(hipMemcpyAsync(d_in, gathered, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    RT_HIP(launch_assemble_rows(d_in, d_out, row_bytes, height, block, n, max_rows, ctx->stream));
+    RT_HIP(hipMemcpyAsync(image, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+rt_status rt_comm_info(const rt_comm* c, int* nranks, int* rank) {
+    if (!c) return fail(RT_ERR_INVALID_ARG, "comm is NULL");
+    if (nranks) *nranks = c->nranks;
+    if (rank) *rank = c->rank;
+    return RT_OK;
+}
+
+}  // extern "C"
