@@ -4,19 +4,26 @@ config 2: 16 spheres + 2 planes + 1 point light, Reinhard tonemap) on 1..N MI355
 
 Contract (driver):  python bench.py --gpus N --steps K --warmup W
   * N=1 runs in-process; N>1 is launched by torch.distributed.run, one rank per GPU.
-  * A step = one pass of the hot path over one frame: Scene::RenderImage() of the C2 frame into
-    the float3 HDR framebuffer + the fused Reinhard tonemap to uint8 (RaytracingEngine.cpp:133),
-    everything resident in HBM (scene uploaded once, outputs stay on the device).
-  * N>1 is weak scaling: every rank renders its own frames (frames are independent, no
-    data-path collective).  `--mode tiled` instead splits ONE frame into row tiles across
-    ranks and assembles it on rank 0 with a gather over RCCL (torch.distributed "nccl").
+  * N=1 (mode "frames"): a step = one pass of the hot path over one frame — Scene::RenderImage()
+    of the C2 frame into the float64 Vec3 framebuffer + the fused Reinhard tonemap to uint8
+    (RaytracingEngine.cpp:133), everything resident in HBM (scene uploaded once, outputs stay
+    on the device).
+  * N>1 (mode "tiled", BASELINE config 4 / SURVEY §8e): a step = ONE 7680×4320 C4 frame split
+    into block-cyclic row sets over the ranks, each rank renders its rows (fused Reinhard
+    uint8), ONE RCCL gather (ncclGather over xGMI, behind the C-ABI: rt_render_gather) moves
+    them to rank 0, and rank 0 assembles the frame in image order in its device framebuffer.
+    Strong scaling; the per-rank render / gather / assembly times are in the line, and the
+    weak-scaling C2 frames throughput is an extra field (`weak_frames`).
   * W untimed steps, then exactly K timed steps bracketed by barrier + synchronize on both
     sides; the max over ranks is the time; rank 0 prints ONE JSON line.
 
-Extra fields: `roofline` (HBM-write bound of the dominant trace kernel from live per-launch HIP
-events; traffic from the committed PMC summary when present), `valu_fp64` (the algorithmic FP64
-flops / time against the FP64 vector peak), `cpu_baseline` (the unmodified reference renderer,
-oracle/_ref, timed on this host's cores; falls back to the C restatement "port").
+Extra fields (N=1): `roofline` (HBM-write bound of the trace kernel from live per-launch HIP
+events; traffic and VALU counters from the committed PMC summaries), `roofline_f32` (the same
+launch with the north star's float3 framebuffer), `moving_camera` (a new camera position every
+frame: no cached per-camera packet image), `d2h` (frames/s of the synchronous host-buffer
+render, the drop-in RenderImage()'s path, pageable and pinned), `tiled_1gpu` (the N>1 default
+workload on one GPU through the same gather path: the strong-scaling anchor), `cpu_baseline`
+(the unmodified reference renderer, oracle/_ref, timed on this host's cores).
 """
 from __future__ import annotations
 
@@ -29,8 +36,9 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (half the FP32 vector rate)
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
+HDR_BYTES = {"f64": 24, "f32": 12}
+GATHER_OUT = {"u8": ("RT_OUT_LDR", 3), "f32": ("RT_OUT_HDR32", 12), "f64": ("RT_OUT_HDR64", 24)}
 
 
 def parse_args(argv=None):
@@ -38,80 +46,89 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", help="c1..c5 (BASELINE configs), mirror, glass, mesh")
-    ap.add_argument("--mode", choices=["frames", "tiled"], default="frames")
+    ap.add_argument("--config", default=None,
+                    help="c1..c5 (BASELINE configs), mirror, glass, mesh; default c2 (frames), "
+                         "c4 (tiled)")
+    ap.add_argument("--mode", choices=["frames", "tiled"], default=None,
+                    help="default: frames at N=1, tiled at N>1")
     ap.add_argument("--tonemap", default="reinhard_simple",
                     help="fused LDR operator, or 'none' (HDR only)")
     ap.add_argument("--row-block", type=int, default=16,
-                    help="tiled mode: rows per block of the block-cyclic split (0: contiguous)")
+                    help="tiled mode: rows per block of the block-cyclic split")
+    ap.add_argument("--gather", choices=sorted(GATHER_OUT), default="u8",
+                    help="tiled mode: the framebuffer each rank renders and rank 0 gathers")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="tiled mode: gather on the render stream (no overlap of frame k's "
+                         "gather with frame k+1's render)")
     ap.add_argument("--hdr", choices=["f64", "f32"], default="f64",
-                    help="HDR framebuffer type: f64 = the reference's std::vector<Vec3> (default)")
+                    help="frames mode HDR framebuffer: f64 = the reference's std::vector<Vec3>")
     ap.add_argument("--event-every", type=int, default=10,
-                    help="bracket every n-th timed launch with HIP events (0: none)")
+                    help="bracket every n-th timed step with HIP events (0: none)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="> 1: also measure K frames with this many in flight on as many "
-                         "streams ('pipelined' field; off by default so that a rocprofv3 "
-                         "summary of the default command is the headline's launches only)")
+                         "streams ('pipelined' field)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="headline only (no f32 / moving-camera / D2H / tiled / weak fields)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=6,
                     help="reference frames timed for cpu_baseline (first one is warm-up)")
     return ap.parse_args(argv)
 
 
-def alg_flops_per_ray(sc) -> int:
-    """F_ray = 25·Ns + 14·Np (+ 30·Nt for Möller–Trumbore)."""
-    return 25 * len(sc.spheres) + 14 * len(sc.planes) + 30 * len(sc.triangle_array())
-
-
-def load_traffic(config: str, mode: str):
-    """Per-launch HBM bytes of the trace kernel from the committed PMC summary, if any."""
-    path = os.path.join(HERE, "profiles", f"pmc_{config}_{mode}.json")
+def load_profile(name: str):
+    path = os.path.join(HERE, "profiles", name)
     if not os.path.exists(path):
         return None, None
     with open(path) as fh:
-        d = json.load(fh)
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, HERE)
+        return json.load(fh), os.path.relpath(path, HERE)
+
+
+def granted_cores() -> int:
+    """Cores this process may run on: the affinity mask, capped by OMP_NUM_THREADS when the
+    environment sets one (the GPU box grants a 16-core share of a larger machine)."""
+    n = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(n, omp) if omp > 0 else n
 
 
 def cpu_baseline(sc, rays_per_frame: int, frames: int):
     """The reference CPU loop on this host: oracle/_ref/ref_harness (unmodified reference
-    Scene::RenderImage, OpenMP on all granted cores), median of frames-1 after one warm-up.
-    Falls back to the C restatement (kind "port") when the reference build is absent."""
+    Scene::RenderImage, OpenMP on the granted cores, threads bound one per core), median of
+    frames-1 after one warm-up, and one frame on one thread.  Falls back to the C restatement
+    (kind "port") when the reference build is absent."""
     from oracle import pyoracle as po
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    if po.ref_available():
-        _, ms, used = po.ref_render(sc, repeat=frames, threads=threads, want_image=False)
-        kind = "reference"
-    else:
+    threads = granted_cores()
+    ref = po.ref_available()
+
+    def run(nthreads, repeat):
+        if ref:
+            _, ms, used = po.ref_render(sc, repeat=repeat, threads=nthreads, want_image=False,
+                                        bind=True)
+            return ms, used
         ms = []
-        for _ in range(frames):
+        for _ in range(repeat):
             t0 = time.perf_counter()
-            po.render(sc, nthreads=threads)
+            po.render(sc, nthreads=nthreads)
             ms.append((time.perf_counter() - t0) * 1e3)
-        used, kind = threads, "port"
+        return ms, nthreads
+
+    ms, used = run(threads, frames)
     timed = sorted(ms[1:] if len(ms) > 1 else ms)
     med = timed[len(timed) // 2]
-    # SURVEY §8d also asks for the one-core figure: one frame after the warm-up above
-    if po.ref_available():
-        _, ms1, _ = po.ref_render(sc, repeat=1, threads=1, want_image=False)
-    else:
-        t0 = time.perf_counter()
-        po.render(sc, nthreads=1)
-        ms1 = [(time.perf_counter() - t0) * 1e3]
-    single = {"value": rays_per_frame / (ms1[0] / 1e3) / 1e6, "cores": 1,
-              "ms_per_frame": ms1[0]}
+    ms1, _ = run(1, 1)
+    single = {"value": rays_per_frame / (ms1[0] / 1e3) / 1e6, "cores": 1, "ms_per_frame": ms1[0]}
     multi = {"value": rays_per_frame / (med / 1e3) / 1e6, "cores": used, "ms_per_frame": med}
-    # The box's granted CPU share can be smaller than the thread count OpenMP is given (its
-    # frames then run slower than one thread's); the baseline is the faster of the two runs.
+    # The reference's chunk-1 dynamic OpenMP loop (Scene.h:318) can run slower on many threads
+    # than on one; the baseline is the faster of the two runs, both are in the line.
     best = multi if multi["value"] >= single["value"] else single
     return {
         "value": best["value"],
         "unit": "Mrays/s",
         "cores": best["cores"],
-        "kind": kind,
+        "kind": "reference" if ref else "port",
         "sample": f"{len(ms)} full {sc.camera.width}x{sc.camera.height} frames of config "
-                  f"{sc.name} on {used} threads (Scene::RenderImage only, first frame warm-up; "
-                  f"median {med:.1f} ms/frame) and one frame on 1 thread "
+                  f"{sc.name} on {used} threads bound to cores (Scene::RenderImage only, first "
+                  f"frame warm-up; median {med:.1f} ms/frame) and one frame on 1 thread "
                   f"({ms1[0]:.1f} ms); value = the faster",
         "ms_per_frame": best["ms_per_frame"],
         "all_threads": multi,
@@ -119,238 +136,398 @@ def cpu_baseline(sc, rays_per_frame: int, frames: int):
     }
 
 
+class Runner:
+    """Per-process state: the rank, a torch stream the library launches on, timing helpers."""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.args = args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus and self.world > 1:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={self.world}")
+        torch.cuda.set_device(self.local_rank)
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+        from raytracingengine_amd import capi
+        self.capi = capi
+        self.ctx = capi.Context(self.local_rank)
+        self.stream = torch.cuda.Stream()
+        self.ctx.set_stream(self.stream.cuda_stream)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max_over_ranks(self, *vals):
+        if self.world == 1:
+            return vals
+        t = self.torch.tensor(vals, dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return tuple(float(x) for x in t)
+
+    def sum_over_ranks(self, *vals):
+        if self.world == 1:
+            return vals
+        t = self.torch.tensor(vals, dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return tuple(float(x) for x in t)
+
+    def gather_rows(self, vals):
+        """Every rank's list of floats, on every rank ([world][len])."""
+        if self.world == 1:
+            return [list(vals)]
+        t = self.torch.tensor(vals, dtype=self.torch.float64, device="cuda")
+        out = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [[float(x) for x in o] for o in out]
+
+    def timed(self, step, steps, warmup, region_events=True):
+        """W untimed steps, then K timed steps between barrier + synchronize; returns
+        (elapsed seconds max over ranks, HIP-event region ms per step on the launch stream)."""
+        torch = self.torch
+        for i in range(warmup):
+            step(i, False)
+        self.barrier()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(self.stream)   # on the stream the trace kernel is launched on
+        for i in range(steps):
+            step(i, True)
+        ev1.record(self.stream)
+        torch.cuda.synchronize()
+        self.barrier()
+        elapsed = time.perf_counter() - t0
+        region_ms = ev0.elapsed_time(ev1) / steps if region_events else None
+        (elapsed,) = self.max_over_ranks(elapsed)
+        return elapsed, region_ms
+
+    def count_rays(self, dscene, opts):
+        """Rays of one render with these options (separate counting launch, never timed)."""
+        capi = self.capi
+        o = capi.default_opts()
+        for f, _ in capi.RenderOpts._fields_:
+            setattr(o, f, getattr(opts, f))
+        o.flags = capi.RT_FLAG_COUNT_RAYS
+        o.tonemap = -1
+        rows = capi.rendered_rows(o, dscene.data.camera.height)
+        W = dscene.data.camera.width
+        buf = self.torch.empty(max(rows, 1) * W * 3, dtype=self.torch.float32, device="cuda")
+        with self.torch.cuda.stream(self.stream):
+            self.ctx.reset_stats()
+            if rows:
+                dscene.render_device(None, buf.data_ptr(), None, o)
+            st = self.ctx.stats()
+            self.ctx.reset_stats()
+        return st.trace_rays + st.shadow_rays
+
+
+# ------------------------------------------------------------------------------ frames mode
+def frames_mode(R: Runner, sc, steps, warmup, hdr="f64", tonemap=1, event_every=10,
+                camera_step=None):
+    """Every rank renders whole frames (weak scaling).  camera_step(i) -> new camera position
+    per frame (moving camera), else a static camera."""
+    torch, capi = R.torch, R.capi
+    W, H = sc.camera.width, sc.camera.height
+    dscene = R.ctx.scene(sc)
+    hdr_t = torch.empty(H * W * 3, dtype=torch.float64 if hdr == "f64" else torch.float32,
+                        device="cuda")
+    ldr = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda") if tonemap >= 0 else None
+    hargs = (hdr_t.data_ptr(), None) if hdr == "f64" else (None, hdr_t.data_ptr())
+    opts = capi.default_opts(tonemap=tonemap)
+    timed_opts = capi.default_opts(tonemap=tonemap, flags=capi.RT_FLAG_TIME_KERNEL)
+    rays = R.count_rays(dscene, opts)
+    base = dscene.camera["position"][0].copy()
+
+    def step(i, timed):
+        if camera_step is not None:
+            dscene.camera["position"][0] = camera_step(base, i if timed else -1 - i)
+        ev = timed and event_every > 0 and i % event_every == 0
+        dscene.render_device(*hargs, ldr.data_ptr() if ldr is not None else None,
+                             timed_opts if ev else opts)
+
+    R.ctx.reset_stats()
+    elapsed, region_ms = R.timed(step, steps, warmup)
+    kst = R.ctx.stats()
+    dscene.camera["position"][0] = base
+    dscene.close()
+    sampled_ms = kst.kernel_ms / kst.launches if kst.launches else None
+    return {"rays": rays, "elapsed": elapsed, "region_ms": region_ms, "sampled_ms": sampled_ms,
+            "px": W * H, "bufs": (hdr_t, ldr)}
+
+
+def pipelined_frames(R: Runner, sc, steps, warmup, inflight, tonemap=1):
+    """The same K frames with `inflight` frames in flight on as many HIP streams, each with its
+    own framebuffers (a serving setup: one frame's tail overlaps the next one's start)."""
+    torch, capi = R.torch, R.capi
+    W, H = sc.camera.width, sc.camera.height
+    dscene = R.ctx.scene(sc)
+    streams = [R.stream] + [torch.cuda.Stream() for _ in range(inflight - 1)]
+    bufs = [(torch.empty(H * W * 3, dtype=torch.float64, device="cuda"),
+             torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")) for _ in streams]
+    opts = capi.default_opts(tonemap=tonemap)
+
+    def step(i, timed):
+        k = i % inflight
+        R.ctx.set_stream(streams[k].cuda_stream)
+        h, l = bufs[k]
+        dscene.render_device(h.data_ptr(), None, l.data_ptr(), opts)
+
+    elapsed, _ = R.timed(step, steps, warmup, region_events=False)
+    R.ctx.set_stream(R.stream.cuda_stream)
+    dscene.close()
+    return elapsed
+
+
+def d2h_frames(R: Runner, sc, frames=20, tonemap=1):
+    """The drop-in RenderImage() path: synchronous rt_render into HOST framebuffers (float64
+    Vec3 + the fused bytes), frames/s including the device-to-host copies — into pageable
+    numpy arrays (a std::vector) and into pinned memory."""
+    import numpy as np
+    torch, capi = R.torch, R.capi
+    W, H = sc.camera.width, sc.camera.height
+    dscene = R.ctx.scene(sc)
+    out = {}
+    pageable = (np.empty((H, W, 3), np.float64), np.empty((H, W, 3), np.uint8))
+    pinned = (torch.empty((H, W, 3), dtype=torch.float64).pin_memory(),
+              torch.empty((H, W, 3), dtype=torch.uint8).pin_memory())
+    o = capi.default_opts(tonemap=tonemap)
+    for kind, (a64, a8) in (("pageable", pageable), ("pinned", pinned)):
+        p64 = a64.ctypes.data if kind == "pageable" else a64.data_ptr()
+        p8 = a8.ctypes.data if kind == "pageable" else a8.data_ptr()
+        for _ in range(3):
+            dscene.render_host(p64, None, p8, o)
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            dscene.render_host(p64, None, p8, o)
+        dt = (time.perf_counter() - t0) / frames
+        out[kind] = {"frames_per_sec": round(1.0 / dt, 2), "ms_per_frame": round(dt * 1e3, 4)}
+    dscene.close()
+    out["bytes_per_frame"] = W * H * 27
+    out["note"] = ("rt_render (synchronous): render + D2H of the float64 Vec3 framebuffer and "
+                   "the Reinhard bytes into host memory, as the drop-in Scene::RenderImage()")
+    return out
+
+
+# ------------------------------------------------------------------------------ tiled mode
+def tiled_mode(R: Runner, sc, steps, warmup, gather="u8", tonemap=1, block=16,
+               event_every=10, pipeline=True):
+    """One frame split over the ranks: block-cyclic rows, one RCCL gather to rank 0, rank 0
+    assembles the frame in image order (rt_render_gather).  Returns per-rank timings."""
+    torch, capi = R.torch, R.capi
+    W, H = sc.camera.width, sc.camera.height
+    if R.world > 1:
+        uid = [capi.comm_unique_id() if R.rank == 0 else None]
+        R.dist.broadcast_object_list(uid, src=0)
+        uid = uid[0]
+    else:
+        uid = capi.comm_unique_id()
+    comm = capi.Comm(R.ctx, R.world, R.rank, uid)
+    dscene = R.ctx.scene(sc)
+    out_name, bpp = GATHER_OUT[gather]
+    outputs = getattr(capi, out_name)
+    dtype = {"u8": torch.uint8, "f32": torch.float32, "f64": torch.float64}[gather]
+    frame = torch.empty(H * W * 3 if R.rank == 0 else 1, dtype=dtype, device="cuda")
+    ptrs = [None, None, None]
+    if R.rank == 0:
+        ptrs[{"f64": 0, "f32": 1, "u8": 2}[gather]] = frame.data_ptr()
+    tm = tonemap if gather == "u8" else -1
+    pf = capi.RT_FLAG_PIPELINE if pipeline else 0
+    opts = capi.default_opts(tonemap=tm, row_block=block, flags=pf)
+    timed_opts = capi.default_opts(tonemap=tm, row_block=block,
+                                   flags=pf | capi.RT_FLAG_TIME_KERNEL)
+    # this rank's rays: its rows of the frame (the gather's plan)
+    plan = capi.default_opts(tonemap=-1)
+    if R.world > 1:
+        plan.row_begin, plan.row_end = R.rank * block, H
+        plan.row_block, plan.row_cycle = block, R.world
+    rays_rank = R.count_rays(dscene, plan) if plan.row_begin < H else 0
+
+    def step(i, timed):
+        ev = timed and event_every > 0 and i % event_every == 0
+        comm.render_gather(dscene, timed_opts if ev else opts, outputs, *ptrs)
+
+    comm.timing(reset=True)
+    elapsed, _ = R.timed(step, steps, warmup, region_events=False)
+    t = comm.timing(reset=True)
+    per = [t.render_ms / max(t.frames, 1), t.gather_ms / max(t.frames, 1),
+           t.assemble_ms / max(t.frames, 1), float(t.rows), float(rays_rank)]
+    ranks = R.gather_rows(per)
+    (rays_all,) = R.sum_over_ranks(float(rays_rank))
+    dscene.close()
+    comm.close()
+    return {"elapsed": elapsed, "rays": rays_all, "ranks": ranks, "px": W * H, "bpp": bpp,
+            "max_rows": t.max_rows, "pipeline": pipeline}
+
+
+def tiled_summary(res, steps, W, gather, block):
+    ranks = res["ranks"]
+    render = [r[0] for r in ranks]
+    mean_render = sum(render) / len(render)
+    return {
+        "per_rank": [{"rank": i, "rows": int(r[3]), "rays": int(r[4]), "render_ms": round(r[0], 5),
+                      "gather_ms": round(r[1], 5), "assemble_ms": round(r[2], 5)}
+                     for i, r in enumerate(ranks)],
+        "render_ms_max": round(max(render), 5),
+        "render_imbalance": round(max(render) / mean_render, 4) if mean_render > 0 else None,
+        "gather_bytes_per_rank": res["max_rows"] * W * res["bpp"],
+        "gathered": gather,
+        "row_block": block,
+        "pipelined": res["pipeline"],
+        "ms_per_frame": round(res["elapsed"] / steps * 1e3, 5),
+        "value": round(res["rays"] * steps / res["elapsed"] / 1e6, 3),
+    }
+
+
+# ------------------------------------------------------------------------------ main
 def main(argv=None):
     args = parse_args(argv)
-    import torch
-    import torch.distributed as dist
-
-    from raytracingengine_amd import capi
+    R = Runner(args)
+    capi = R.capi
     from raytracingengine_amd.configs import make_config
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
+    mode = args.mode or ("frames" if R.world == 1 else "tiled")
+    config = args.config or ("c2" if mode == "frames" else "c4")
     tonemap = -1 if args.tonemap == "none" else capi.TONEMAPS.index(args.tonemap)
-    sc = make_config(args.config, aa=1)
+    sc = make_config(config, aa=1)
     W, H = sc.camera.width, sc.camera.height
-    ctx = capi.Context(local_rank)
-    stream = torch.cuda.Stream()
-    ctx.set_stream(stream.cuda_stream)
-    dscene = ctx.scene(sc)
+    line = None
+    extras = not args.no_extras
 
-    from raytracingengine_amd.distributed import plan_rows, render_opts_for, row_ranges
-    # frames: the whole image; tiled: this rank's rows of the one frame, dealt in
-    # blocks of --row-block rows round-robin (contiguous tiles of C3/C4 are 1.7x imbalanced)
-    block = args.row_block if args.mode == "tiled" else 0
-    nparts = world if args.mode == "tiled" else 1
-    plans = [row_ranges(r, nparts, H, block) for r in range(nparts)]
-    my_plan = plans[rank if args.mode == "tiled" else 0]
-    rows = plan_rows(my_plan)
-    max_rows = max(plan_rows(p) for p in plans)  # the gather moves equal-sized buffers
-
-    def make_opts(**kw):
-        return render_opts_for(my_plan, rank if args.mode == "tiled" else 0, nparts, H, block,
-                               **kw)
-
-    hdr_dtype = torch.float64 if args.hdr == "f64" else torch.float32
-    hdr = torch.zeros(max_rows * W * 3, dtype=hdr_dtype, device="cuda")
-    ldr = torch.empty(rows * W * 3, dtype=torch.uint8, device="cuda") if tonemap >= 0 else None
-    def hdr_args():
-        return (hdr.data_ptr(), None) if args.hdr == "f64" else (None, hdr.data_ptr())
-
-    full = perm = None
-    if args.mode == "tiled" and world > 1 and rank == 0:
-        full = [torch.empty(max_rows * W * 3, dtype=hdr_dtype, device="cuda") for _ in range(world)]
-        # frame row y <- row perm[y] of the concatenated per-rank buffers
-        order = [0] * H
-        for r, plan in enumerate(plans):
-            k = r * max_rows
-            for a, b in plan:
-                for y in range(a, b):
-                    order[y] = k
-                    k += 1
-        perm = torch.tensor(order, dtype=torch.long, device="cuda")
-
-    # ray counts of this rank's pixels (separate counting launch, not timed)
-    with torch.cuda.stream(stream):
-        ctx.reset_stats()
-        dscene.render_device(*hdr_args(), None,
-                             make_opts(tonemap=-1, flags=capi.RT_FLAG_COUNT_RAYS))
-        st = ctx.stats()
-    rays_rank = st.trace_rays + st.shadow_rays
-    ctx.reset_stats()
-
-    opts = make_opts(tonemap=tonemap)
-    timed_opts = make_opts(tonemap=tonemap, flags=capi.RT_FLAG_TIME_KERNEL)
-
-    def step(o):
-        dscene.render_device(*hdr_args(), ldr.data_ptr() if ldr is not None else None, o)
-        if args.mode == "tiled" and world > 1:
-            with torch.cuda.stream(stream):
-                dist.gather(hdr, full if rank == 0 else None, dst=0)
-                if rank == 0:  # assemble: rows back into image order (one device gather)
-                    frame = torch.cat(full).view(world * max_rows, W * 3).index_select(0, perm)
-                    del frame
-
-    for _ in range(args.warmup):
-        step(opts)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)   # on the stream the trace kernel is launched on
-    for i in range(args.steps):
-        ev = args.event_every > 0 and i % args.event_every == 0
-        step(timed_opts if ev else opts)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    region_ms = ev0.elapsed_time(ev1) / args.steps
-    elapsed = t1 - t0
-    kst = ctx.stats()
-
-    # Serving note (frames mode): the same K frames with two frames in flight on two streams
-    # (each with its own framebuffers), so one frame's tail overlaps the next one's start.
-    # Reported beside the headline, not as it: per-launch durations overlap there.
-    pipelined = None
-    if args.mode == "frames" and args.inflight > 1:
-        streams = [stream] + [torch.cuda.Stream() for _ in range(args.inflight - 1)]
-        bufs = [(hdr, ldr)] + [
-            (torch.empty_like(hdr), torch.empty_like(ldr) if ldr is not None else None)
-            for _ in range(args.inflight - 1)]
-
-        def step_on(k, o):
-            ctx.set_stream(streams[k].cuda_stream)
-            h, l = bufs[k]
-            args_h = (h.data_ptr(), None) if args.hdr == "f64" else (None, h.data_ptr())
-            dscene.render_device(*args_h, l.data_ptr() if l is not None else None, o)
-
-        for i in range(args.warmup):
-            step_on(i % args.inflight, opts)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        p0 = time.perf_counter()
-        for i in range(args.steps):
-            step_on(i % args.inflight, opts)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        p_el = time.perf_counter() - p0
-        ctx.set_stream(stream.cuda_stream)
-        if world > 1:
-            t = torch.tensor([p_el], dtype=torch.float64, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            p_el = float(t[0])
-        pipelined = (p_el, args.inflight)
-    # sampled per-launch events (every --event-every-th launch, bracketing the kernel alone)
-    sampled_ms = kst.kernel_ms / kst.launches if kst.launches else None
-    # frames mode: the kernel is the only work on the stream, so the region average is the
-    # launch duration including the back-to-back dispatch gap (agrees with rocprofv3 within a
-    # few %); tiled mode also runs the gather there, so the sampled launches are used.
-    kernel_ms = region_ms if args.mode == "frames" or sampled_ms is None else sampled_ms
-
-    if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
-        r = torch.tensor([rays_rank], dtype=torch.float64, device="cuda")
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        rays_all = float(r[0])
-    else:
-        rays_all = float(rays_rank)
-
-    if args.mode == "frames":
-        total_rays = rays_all * args.steps          # every rank renders a full frame per step
-        frames = world * args.steps
-    else:
-        total_rays = rays_all * args.steps          # the ranks together render one frame
-        frames = args.steps
-    value = total_rays / elapsed / 1e6
-
-    if rank == 0:
-        px = rows * W
-        hdr_bytes = 24 if args.hdr == "f64" else 12
-        bytes_per_launch = px * (hdr_bytes + (3 if tonemap >= 0 else 0))  # Vec3 HDR + u8 LDR
+    if mode == "frames":
+        res = frames_mode(R, sc, args.steps, args.warmup, args.hdr, tonemap, args.event_every)
+        elapsed, rays_rank = res["elapsed"], res["rays"]
+        (kernel_ms,) = R.max_over_ranks(res["region_ms"])
+        (rays_all,) = R.sum_over_ranks(float(rays_rank))
+        value = rays_all * args.steps / elapsed / 1e6
+        frames = R.world * args.steps
+        bytes_per_launch = res["px"] * (HDR_BYTES[args.hdr] + (3 if tonemap >= 0 else 0))
         achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9
-        traffic, traffic_src = load_traffic(args.config, args.mode)
-        flops = rays_rank * alg_flops_per_ray(sc)
+        traffic, traffic_src = load_profile(f"pmc_{config}_frames.json")
+        valu, valu_src = load_profile(f"r02_{config}_valu.json")
         line = {
-            "metric": "Mrays/sec (primary+shadow) at 1920x1080" if args.config == "c2"
-                      else f"Mrays/sec (primary+shadow), config {args.config}",
-            "value": round(value, 3),
-            "unit": "Mrays/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
+            "metric": "Mrays/sec (primary+shadow) at 1920x1080" if config == "c2"
+                      else f"Mrays/sec (primary+shadow), config {config}",
+            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": R.world,
+            "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True,
-            "scaling": "weak" if args.mode == "frames" else "strong",
-            "vs_baseline": None,
-            "dtype": "f64",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"{args.config}: {W}x{H}, {len(sc.spheres)} spheres, "
-                            f"{len(sc.planes)} planes, {len(sc.lights)} point lights, AA=1, "
-                            f"{args.hdr} Vec3 HDR framebuffer + fused {args.tonemap} u8",
-                "global_batch": frames,
-                "resolution": [W, H],
-                "parallelism": (f"frames x{world}" if args.mode == "frames"
-                                else f"block-cyclic rows ({block}-row blocks) x{world} + "
-                                     f"RCCL gather"),
-                "rays_per_frame": rays_all if args.mode == "tiled" else rays_rank,
+                "workload": f"{config}: {W}x{H}, {len(sc.spheres)} spheres, {len(sc.planes)} "
+                            f"planes, {len(sc.lights)} point lights, AA=1, {args.hdr} Vec3 HDR "
+                            f"framebuffer + fused {args.tonemap} u8, static camera",
+                "global_batch": frames, "resolution": [W, H],
+                "parallelism": f"frames x{R.world}", "rays_per_frame": rays_rank,
             },
             "frames_per_sec": round(frames / elapsed, 3),
             "kernel_ms_per_launch": round(kernel_ms, 6),
-            "kernel_ms_sampled_events": round(sampled_ms, 6) if sampled_ms else None,
+            "kernel_ms_sampled_events": round(res["sampled_ms"], 6) if res["sampled_ms"] else None,
             "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic,
-                "alg_bytes_per_launch": bytes_per_launch,
-                "traffic_source": traffic_src,
+                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+                "alg_bytes_per_launch": bytes_per_launch, "traffic_source": traffic_src,
             },
-            "valu_fp64": {
-                "achieved": round(flops / (kernel_ms / 1e3) / 1e12, 3),
-                "peak": FP64_VALU_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(flops / (kernel_ms / 1e3) / 1e12 / FP64_VALU_PEAK_TFLOPS, 5),
-                "alg_flops_per_launch": flops,
-            },
+            "valu": valu, "valu_source": valu_src,
             "cpu_baseline": None,
         }
-        if pipelined is not None:
-            p_el, nin = pipelined
-            line["pipelined"] = {
-                "inflight": nin, "streams": nin,
-                "value": round(rays_all * args.steps / p_el / 1e6, 3),
-                "ms_per_step": round(p_el / args.steps * 1e3, 5),
-                "note": "same K frames, two in flight on two HIP streams (serving throughput); "
-                        "not the headline value",
-            }
-        if world == 1 and not args.no_cpu_baseline:
+        if extras and R.world == 1:
+            steps_x = min(args.steps, 100)
+            # the north star's float3 framebuffer (+ u8): 15 B/px instead of 27
+            f32 = frames_mode(R, sc, steps_x, args.warmup, "f32", tonemap, 0)
+            b32 = f32["px"] * (12 + (3 if tonemap >= 0 else 0))
+            a32 = b32 / (f32["region_ms"] / 1e3) / 1e9
+            line["roofline_f32"] = {
+                "achieved": round(a32, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(a32 / HBM_PEAK_GBS, 5), "alg_bytes_per_launch": b32,
+                "kernel_ms_per_launch": round(f32["region_ms"], 6),
+                "value": round(f32["rays"] * steps_x / f32["elapsed"] / 1e6, 3)}
+            # a camera that moves every frame: never the cached per-camera packet image
+            mv = frames_mode(R, sc, steps_x, args.warmup, args.hdr, tonemap, 0,
+                             camera_step=lambda base, i: base + (i * 1e-7, 0.0, 0.0))
+            line["moving_camera"] = {
+                "ms_per_step": round(mv["elapsed"] / steps_x * 1e3, 5),
+                "kernel_ms_per_launch": round(mv["region_ms"], 6),
+                "value": round(mv["rays"] * steps_x / mv["elapsed"] / 1e6, 3),
+                "note": "camera x moved by 1e-7 every frame: the per-camera packet image is "
+                        "never reused; rays counted at the first position"}
+            if args.inflight > 1:
+                el = pipelined_frames(R, sc, args.steps, args.warmup, args.inflight, tonemap)
+                line["pipelined"] = {
+                    "inflight": args.inflight,
+                    "value": round(rays_rank * args.steps / el / 1e6, 3),
+                    "ms_per_step": round(el / args.steps * 1e3, 5),
+                    "note": "same K frames in flight on several HIP streams (serving "
+                            "throughput); not the headline value"}
+            line["d2h"] = d2h_frames(R, sc, min(args.steps, 20), tonemap)
+            # the N>1 default workload (C4 tiled + RCCL gather) on this one GPU
+            sc4 = make_config("c4", aa=1)
+            t1 = tiled_mode(R, sc4, min(args.steps, 20), min(args.warmup, 3), "u8", 1,
+                            args.row_block, 1, not args.no_pipeline)
+            line["tiled_1gpu"] = tiled_summary(t1, min(args.steps, 20), sc4.camera.width, "u8",
+                                               args.row_block)
+            line["tiled_1gpu"]["workload"] = ("c4 7680x4320, 256 spheres, 8 lights, Reinhard "
+                                              "u8 through rt_render_gather on 1 rank")
+        if R.world == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(sc, rays_rank, args.cpu_frames)
             except Exception as e:  # a reported baseline, never the product path
                 line["cpu_baseline"] = {"error": repr(e)}
+    else:
+        res = tiled_mode(R, sc, args.steps, args.warmup, args.gather, tonemap, args.row_block,
+                         args.event_every, not args.no_pipeline)
+        summ = tiled_summary(res, args.steps, W, args.gather, args.row_block)
+        elapsed = res["elapsed"]
+        value = res["rays"] * args.steps / elapsed / 1e6
+        r0 = res["ranks"][0]
+        bytes_rank0 = int(r0[3]) * W * res["bpp"]
+        achieved = bytes_rank0 / (r0[0] / 1e3) / 1e9 if r0[0] > 0 else 0.0
+        line = {
+            "metric": "Mrays/sec (primary+shadow), row-tiled frame + RCCL gather",
+            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": R.world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{config}: {W}x{H}, {len(sc.spheres)} spheres, {len(sc.planes)} "
+                            f"planes, {len(sc.lights)} point lights, AA=1, one frame per step "
+                            f"split over {R.world} GPUs, fused {args.tonemap} {args.gather} "
+                            f"gathered to rank 0",
+                "global_batch": args.steps, "resolution": [W, H],
+                "parallelism": f"block-cyclic rows ({args.row_block}-row blocks) x{R.world} + "
+                               f"one ncclGather per frame",
+                "rays_per_frame": res["rays"],
+            },
+            "frames_per_sec": round(args.steps / elapsed, 3),
+            "tiled": summ,
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "alg_bytes_per_launch": bytes_rank0,
+                "note": "rank 0's render launch: its rows' framebuffer bytes / render time",
+            },
+            "cpu_baseline": None,
+        }
+        if extras:
+            sc2 = make_config("c2", aa=1)
+            wk = frames_mode(R, sc2, args.steps, args.warmup, "f64", tonemap, 0)
+            (rays2,) = R.sum_over_ranks(float(wk["rays"]))
+            line["weak_frames"] = {
+                "value": round(rays2 * args.steps / wk["elapsed"] / 1e6, 3),
+                "ms_per_step": round(wk["elapsed"] / args.steps * 1e3, 5),
+                "workload": "c2 1920x1080 frames, every rank its own (f64 Vec3 + Reinhard u8)",
+                "scaling": "weak"}
+    if R.rank == 0:
         print(json.dumps(line), flush=True)
-
-    dscene.close()
-    ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    R.ctx.close()
+    if R.world > 1:
+        R.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -162,6 +162,9 @@ typedef struct rt_render_opts {
 #define RT_FLAG_TIME_KERNEL 0x2  /* bracket each render launch with HIP events              */
 #define RT_FLAG_GENERIC_KERNEL 0x4 /* ablation: bypass the packet-culled kernel              */
 #define RT_FLAG_NO_BVH 0x8         /* ablation: test every triangle (no triangle BVH)          */
+#define RT_FLAG_PIPELINE 0x10      /* rt_render_gather: gather + assembly on the communicator's
+                                      own stream, overlapping the next frame's render (two
+                                      frame slots); rt_comm_synchronize waits for the frame   */
 
 /* Fills opts with the reference defaults: max_recursion 10, bias 1e-3, tonemap ACES,
  * full image, seed 0x5EED, no flags. */
@@ -262,6 +265,8 @@ rt_status rt_render_gather(rt_comm* comm, const rt_scene* scene, const rt_camera
 rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, int n,
                                const rt_camera* cam, const rt_render_opts* opts, int outputs,
                                void* d_hdr64, void* d_hdr32, void* d_ldr);
+/* Waits for every frame enqueued on the communicator (render, gather, assembly). */
+rt_status rt_comm_synchronize(rt_comm* comm);
 /* Summed frame timings since the last reset (waits for the timed frames to finish). */
 rt_status rt_comm_timing(rt_comm* comm, rt_gather_timing* out, int reset);
 

@@ -147,7 +147,8 @@ def ref_available() -> bool:
     return os.path.exists(REF_HARNESS)
 
 
-def ref_render(sc: SceneData, repeat: int = 1, threads: int | None = None, want_image=True):
+def ref_render(sc: SceneData, repeat: int = 1, threads: int | None = None, want_image=True,
+               bind: bool = False):
     """Run the unmodified reference Scene::RenderImage on `sc`.  Returns (hdr or None, ms list,
     threads).  AA>1 renders are non-deterministic in the reference (random_device seed)."""
     if not ref_available():
@@ -159,6 +160,9 @@ def ref_render(sc: SceneData, repeat: int = 1, threads: int | None = None, want_
         env = dict(os.environ)
         if threads is not None:
             env["OMP_NUM_THREADS"] = str(threads)
+        if bind:  # OpenMP threads pinned to neighbouring cores (one per core)
+            env["OMP_PROC_BIND"] = "close"
+            env["OMP_PLACES"] = "cores"
         res = subprocess.run([REF_HARNESS, "render", scene_path, out_path, str(repeat)],
                              check=True, capture_output=True, text=True, env=env)
         info = json.loads(res.stdout.strip().splitlines()[-1])

@@ -29,6 +29,7 @@ RT_FLAG_COUNT_RAYS = 0x1
 RT_FLAG_TIME_KERNEL = 0x2
 RT_FLAG_GENERIC_KERNEL = 0x4
 RT_FLAG_NO_BVH = 0x8
+RT_FLAG_PIPELINE = 0x10
 RT_OUT_HDR64, RT_OUT_HDR32, RT_OUT_LDR = 0x1, 0x2, 0x4
 RT_COMM_ID_BYTES = 128
 
@@ -39,7 +40,7 @@ EXPORTED = [
     "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
     "rt_render_multi", "rt_comm_unique_id", "rt_comm_create", "rt_comm_create_all",
     "rt_comm_destroy", "rt_comm_info", "rt_render_gather", "rt_render_gather_all",
-    "rt_comm_timing", "rt_debug_assemble_rows",
+    "rt_comm_timing", "rt_comm_synchronize", "rt_debug_assemble_rows",
     "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
     "rt_debug_f64_ops", "rt_debug_vec_ops",
 ]
@@ -134,6 +135,7 @@ def load_library(path: str = LIB_PATH):
         "rt_render_gather": [vp, vp, vp, vp, i32, vp, vp, vp],
         "rt_render_gather_all": [vp, vp, i32, vp, vp, i32, vp, vp, vp],
         "rt_comm_timing": [vp, vp, i32],
+        "rt_comm_synchronize": [vp],
         "rt_debug_assemble_rows": [vp, vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
                                    ctypes.c_uint32, ctypes.c_uint32, vp],
     }.items():
@@ -311,6 +313,15 @@ class DeviceScene:
             out["shadow_rays"] = st.shadow_rays
         return out
 
+    def render_host(self, h_hdr64: int | None, h_hdr32: int | None, h_ldr: int | None,
+                    opts: RenderOpts, stats: bool = False):
+        """Synchronous render into caller-owned HOST buffers (rt_render): the drop-in
+        RenderImage() path, device-to-host copies included."""
+        st = Stats()
+        _check(_lib.rt_render(self.ctx.handle, self._h, self.camera.ctypes.data, ctypes.byref(opts),
+                              h_hdr64, h_hdr32, h_ldr, ctypes.byref(st) if stats else None))
+        return st if stats else None
+
     def trace_rays(self, rays: np.ndarray, stats=False, **opt_kw):
         """Batch TraceRay at depth 0 (rt_trace_rays): rays [n,6] -> rgb [n,3]."""
         rays = np.ascontiguousarray(rays, np.float64).reshape(-1, 6)
@@ -364,6 +375,26 @@ def render_multi(scenes: list, *, hdr64=True, tonemap: int = TONEMAP_NONE, stats
     return out
 
 
+class _StdoutToStderr:
+    """RCCL prints its version banner to stdout when a communicator is created; a bench's
+    stdout carries exactly one JSON line, so the banner goes to stderr instead (fd level, C
+    stdio flushed on both sides)."""
+
+    def __enter__(self):
+        import sys
+        sys.stdout.flush()
+        self._libc = ctypes.CDLL(None)
+        self._libc.fflush(None)
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        self._libc.fflush(None)
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+
+
 def comm_unique_id() -> bytes:
     """ncclGetUniqueId (rt_comm_unique_id): made on one rank, handed to all of them."""
     buf = (ctypes.c_uint8 * RT_COMM_ID_BYTES)()
@@ -386,7 +417,9 @@ class Comm:
         if len(uid) != RT_COMM_ID_BYTES:
             raise ValueError("unique id must be RT_COMM_ID_BYTES bytes")
         idbuf = (ctypes.c_uint8 * RT_COMM_ID_BYTES).from_buffer_copy(uid)
-        _check(L.rt_comm_create(ctx.handle, nranks, rank, idbuf, ctypes.byref(self._h)))
+        with _StdoutToStderr():
+            st = L.rt_comm_create(ctx.handle, nranks, rank, idbuf, ctypes.byref(self._h))
+        _check(st)
 
     @classmethod
     def create_all(cls, ctxs: list) -> list:
@@ -394,7 +427,9 @@ class Comm:
         n = len(ctxs)
         hs = (ctypes.c_void_p * n)(*[c.handle for c in ctxs])
         out = (ctypes.c_void_p * n)()
-        _check(load_library().rt_comm_create_all(hs, n, out))
+        with _StdoutToStderr():
+            st = load_library().rt_comm_create_all(hs, n, out)
+        _check(st)
         return [cls(c, n, i, b"", _handle=ctypes.c_void_p(out[i])) for i, c in enumerate(ctxs)]
 
     @property
@@ -419,6 +454,9 @@ class Comm:
         assembly into the d_* device framebuffers) on the context's stream."""
         _check(_lib.rt_render_gather(self._h, dscene._h, dscene.camera.ctypes.data,
                                      ctypes.byref(opts), outputs, d_hdr64, d_hdr32, d_ldr))
+
+    def synchronize(self):
+        _check(_lib.rt_comm_synchronize(self._h))
 
     def timing(self, reset: bool = False) -> GatherTiming:
         t = GatherTiming()

@@ -30,16 +30,23 @@ hipError_t launch_assemble_rows(const void* gathered, void* image, size_t row_by
 static_assert(RT_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "rt_capi.h id size");
 
 struct rt_comm {
-    rt_context* ctx = nullptr;  // the context whose device and stream the collectives use
+    rt_context* ctx = nullptr;  // the context whose device and stream the renders use
     int device = -1;
     ncclComm_t nccl = nullptr;
     int nranks = 1, rank = 0;
-    // per output kind (RT_OUT_HDR64, _HDR32, _LDR): this rank's packed rows (send), and on
-    // rank 0 the n gathered buffers (recv)
-    DeviceBuffer send[3], recv[3];
-    // RT_FLAG_TIME_KERNEL frames: events before the render, after it, after the gather and
-    // after the assembly
-    struct Ev { hipEvent_t e[4]; };
+    // Two frame slots (RT_FLAG_PIPELINE alternates them; otherwise slot 0).  Per slot and output
+    // kind (RT_OUT_HDR64, _HDR32, _LDR): this rank's packed rows (send) and, on rank 0, the n
+    // gathered buffers (recv).
+    DeviceBuffer send[2][3], recv[2][3];
+    // RT_FLAG_PIPELINE: the gather + assembly run on this stream, overlapping the next frame's
+    // render on the context stream; `rendered` hands a slot to it, `freed` hands it back.
+    hipStream_t gstream = nullptr;
+    hipEvent_t rendered[2] = {nullptr, nullptr}, freed[2] = {nullptr, nullptr};
+    bool slot_used[2] = {false, false};
+    uint64_t frame = 0;
+    // RT_FLAG_TIME_KERNEL frames: before / after the render (context stream), before / after
+    // the gather and after the assembly (gather stream)
+    struct Ev { hipEvent_t e[5]; };
     std::vector<Ev> pending, spare;
     double render_ms = 0, gather_ms = 0, assemble_ms = 0;
     uint64_t frames = 0;
@@ -103,12 +110,12 @@ rt_status check_outputs(int outputs) {
 rt_status harvest(rt_comm* c, bool all) {
     size_t done = 0;
     for (auto& ev : c->pending) {
-        if (!all && hipEventQuery(ev.e[3]) != hipSuccess) break;
-        RT_HIP(hipEventSynchronize(ev.e[3]));
+        if (!all && hipEventQuery(ev.e[4]) != hipSuccess) break;
+        RT_HIP(hipEventSynchronize(ev.e[4]));
         float a = 0, b = 0, d = 0;
         RT_HIP(hipEventElapsedTime(&a, ev.e[0], ev.e[1]));
-        RT_HIP(hipEventElapsedTime(&b, ev.e[1], ev.e[2]));
-        RT_HIP(hipEventElapsedTime(&d, ev.e[2], ev.e[3]));
+        RT_HIP(hipEventElapsedTime(&b, ev.e[2], ev.e[3]));
+        RT_HIP(hipEventElapsedTime(&d, ev.e[3], ev.e[4]));
         c->render_ms += a;
         c->gather_ms += b;
         c->assemble_ms += d;
@@ -120,29 +127,42 @@ rt_status harvest(rt_comm* c, bool all) {
     return RT_OK;
 }
 
-rt_status record(rt_comm* c, rt_comm::Ev* ev, int k) {
+// One frame's state on one rank between the phases.
+struct Frame {
+    Plan pl;
+    rt_comm::Ev* ev = nullptr;
+    int slot = 0;
+    bool pipelined = false;
+    hipStream_t gs = nullptr;  // the stream of the gather and the assembly
+};
+
+rt_status record(rt_comm::Ev* ev, int k, hipStream_t s) {
     if (!ev) return RT_OK;
-    RT_HIP(hipEventRecord(ev->e[k], c->ctx->stream));
+    RT_HIP(hipEventRecord(ev->e[k], s));
     return RT_OK;
 }
 
 // Phase 1 of a frame on one rank: this rank's rows rendered into its send buffers.
 rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
-                      const rt_render_opts* opts, int outputs, Plan& pl, rt_comm::Ev*& ev) {
+                      const rt_render_opts* opts, int outputs, Frame& f) {
     rt_context* ctx = c->ctx;
     if (sc->ctx != ctx)
         return fail(RT_ERR_INVALID_ARG, "scene does not belong to the communicator's context");
-    rt_status st = make_plan(cam, opts, c->nranks, c->rank, pl);
+    rt_status st = make_plan(cam, opts, c->nranks, c->rank, f.pl);
     if (st != RT_OK) return st;
+    Plan& pl = f.pl;
+    f.pipelined = (pl.opts.flags & RT_FLAG_PIPELINE) != 0;
+    f.slot = f.pipelined ? static_cast<int>(c->frame & 1) : 0;
+    f.gs = f.pipelined ? c->gstream : ctx->stream;
     const size_t npx = static_cast<size_t>(pl.max_rows) * cam->width;
     for (int k = 0; k < 3; ++k) {
         if (!(outputs & kOutputs[k])) continue;
-        RT_HIP(c->send[k].ensure(npx * bytes_per_px(k)));
-        if (c->rank == 0) RT_HIP(c->recv[k].ensure(npx * bytes_per_px(k) * c->nranks));
+        RT_HIP(c->send[f.slot][k].ensure(npx * bytes_per_px(k)));
+        if (c->rank == 0) RT_HIP(c->recv[f.slot][k].ensure(npx * bytes_per_px(k) * c->nranks));
     }
     c->rows = pl.rows;
     c->max_rows = pl.max_rows;
-    ev = nullptr;
+    f.ev = nullptr;
     if (pl.opts.flags & RT_FLAG_TIME_KERNEL) {
         if (c->pending.size() >= 256) {
             st = harvest(c, false);
@@ -156,51 +176,81 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
         } else {
             for (auto& x : e.e) RT_HIP(hipEventCreate(&x));
         }
-        ev = &e;
+        f.ev = &e;
     }
     // the frame's own events replace the per-launch ones of the render
-    pl.opts.flags &= ~RT_FLAG_TIME_KERNEL;
+    pl.opts.flags &= ~(RT_FLAG_TIME_KERNEL | RT_FLAG_PIPELINE);
     if (!(outputs & RT_OUT_LDR)) pl.opts.tonemap = RT_TONEMAP_NONE;
     else if (pl.opts.tonemap == RT_TONEMAP_NONE)
         return fail(RT_ERR_INVALID_ARG, "RT_OUT_LDR needs opts->tonemap");
-    st = record(c, ev, 0);
+    // the slot's buffers (and, for a serial frame, the caller's framebuffers) may still be in
+    // use by an earlier pipelined frame's gather / assembly
+    for (int s = 0; s < 2; ++s)
+        if (c->slot_used[s] && (s == f.slot || !f.pipelined))
+            RT_HIP(hipStreamWaitEvent(ctx->stream, c->freed[s], 0));
+    st = record(f.ev, 0, ctx->stream);
     if (st != RT_OK) return st;
     if (pl.rows > 0) {
+        DeviceBuffer* sb = c->send[f.slot];
         st = enqueue_render(ctx, sc, cam, &pl.opts,
-                            (outputs & RT_OUT_HDR64) ? static_cast<double*>(c->send[0].ptr) : nullptr,
-                            (outputs & RT_OUT_HDR32) ? static_cast<float*>(c->send[1].ptr) : nullptr,
-                            (outputs & RT_OUT_LDR) ? static_cast<uint8_t*>(c->send[2].ptr) : nullptr);
+                            (outputs & RT_OUT_HDR64) ? static_cast<double*>(sb[0].ptr) : nullptr,
+                            (outputs & RT_OUT_HDR32) ? static_cast<float*>(sb[1].ptr) : nullptr,
+                            (outputs & RT_OUT_LDR) ? static_cast<uint8_t*>(sb[2].ptr) : nullptr);
         if (st != RT_OK) return st;
     }
-    return record(c, ev, 1);
+    st = record(f.ev, 1, ctx->stream);
+    if (st != RT_OK) return st;
+    if (f.pipelined) {
+        RT_HIP(hipEventRecord(c->rendered[f.slot], ctx->stream));
+        RT_HIP(hipStreamWaitEvent(f.gs, c->rendered[f.slot], 0));
+    }
+    return record(f.ev, 2, f.gs);
 }
 
-// Phase 2: one ncclGather per output (inside the caller's group when several are issued).
-rt_status gather_part(rt_comm* c, const rt_camera* cam, int outputs, const Plan& pl) {
-    const size_t npx = static_cast<size_t>(pl.max_rows) * cam->width;
+// Phase 2: one ncclGather per output (inside the caller's group).
+rt_status gather_part(rt_comm* c, const rt_camera* cam, int outputs, const Frame& f) {
+    const size_t npx = static_cast<size_t>(f.pl.max_rows) * cam->width;
     for (int k = 0; k < 3; ++k) {
         if (!(outputs & kOutputs[k])) continue;
-        void* recv = c->rank == 0 ? c->recv[k].ptr : c->send[k].ptr;
-        RT_NCCL(ncclGather(c->send[k].ptr, recv, npx * bytes_per_px(k), ncclUint8, 0, c->nccl,
-                           c->ctx->stream));
+        void* send = c->send[f.slot][k].ptr;
+        void* recv = c->rank == 0 ? c->recv[f.slot][k].ptr : send;
+        RT_NCCL(ncclGather(send, recv, npx * bytes_per_px(k), ncclUint8, 0, c->nccl, f.gs));
     }
     return RT_OK;
 }
 
 // Phase 3 (rank 0): gathered rows into image order in the caller's device framebuffers.
-rt_status assemble_part(rt_comm* c, const rt_camera* cam, int outputs, const Plan& pl,
-                        void* const* dst, rt_comm::Ev* ev) {
-    rt_status st = record(c, ev, 2);
+rt_status assemble_part(rt_comm* c, const rt_camera* cam, int outputs, const Frame& f,
+                        void* const* dst) {
+    rt_status st = record(f.ev, 3, f.gs);
     if (st != RT_OK) return st;
     if (c->rank == 0) {
         for (int k = 0; k < 3; ++k) {
             if (!(outputs & kOutputs[k]) || !dst[k]) continue;
-            RT_HIP(launch_assemble_rows(c->recv[k].ptr, dst[k], size_t(cam->width) * bytes_per_px(k),
-                                        cam->height, pl.block, static_cast<uint32_t>(c->nranks),
-                                        pl.max_rows, c->ctx->stream));
+            RT_HIP(launch_assemble_rows(c->recv[f.slot][k].ptr, dst[k],
+                                        size_t(cam->width) * bytes_per_px(k), cam->height,
+                                        f.pl.block, static_cast<uint32_t>(c->nranks),
+                                        f.pl.max_rows, f.gs));
         }
     }
-    return record(c, ev, 3);
+    st = record(f.ev, 4, f.gs);
+    if (st != RT_OK) return st;
+    if (f.pipelined) {
+        RT_HIP(hipEventRecord(c->freed[f.slot], f.gs));
+        c->slot_used[f.slot] = true;
+    }
+    c->frame += 1;
+    return RT_OK;
+}
+
+// The gather stream and the slot hand-over events (the caller holds a DeviceGuard).
+rt_status init_streams(rt_comm* c) {
+    RT_HIP(hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
+    for (int s = 0; s < 2; ++s) {
+        RT_HIP(hipEventCreateWithFlags(&c->rendered[s], hipEventDisableTiming));
+        RT_HIP(hipEventCreateWithFlags(&c->freed[s], hipEventDisableTiming));
+    }
+    return RT_OK;
 }
 
 rt_status check_root_outputs(const rt_comm* c, int outputs, void* const* dst) {
@@ -451,11 +501,16 @@ rt_status rt_comm_create(rt_context* ctx, int nranks, int rank, const uint8_t* i
     c->device = ctx->device;
     c->nranks = nranks;
     c->rank = rank;
+    rt_status st = init_streams(c);
+    if (st != RT_OK) {
+        rt_comm_destroy(c);
+        return st;
+    }
     ncclUniqueId u;
     std::memcpy(u.internal, id, sizeof u.internal);
     const ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, u, rank);
     if (r != ncclSuccess) {
-        delete c;
+        rt_comm_destroy(c);
         return nccl_fail(r, "ncclCommInitRank");
     }
     *out = c;
@@ -491,6 +546,13 @@ rt_status rt_comm_create_all(rt_context* const* ctxs, int n, rt_comm** out) {
         c->nranks = n;
         c->rank = i;
         out[i] = c;
+        DeviceGuard g(devs[i]);
+        rt_status st = init_streams(c);
+        if (st != RT_OK) {
+            for (int j = 0; j <= i; ++j) rt_comm_destroy(out[j]);
+            for (int j = i + 1; j < n; ++j) (void)ncclCommDestroy(comms[j]);
+            return st;
+        }
     }
     return RT_OK;
 }
@@ -499,15 +561,29 @@ rt_status rt_comm_destroy(rt_comm* c) {
     if (!c) return RT_OK;
     DeviceGuard g(c->device);
     if (c->ctx && c->ctx->stream) (void)hipStreamSynchronize(c->ctx->stream);
+    if (c->gstream) (void)hipStreamSynchronize(c->gstream);
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
     for (auto* v : {&c->pending, &c->spare})
         for (auto& ev : *v)
             for (auto& x : ev.e) (void)hipEventDestroy(x);
-    for (int k = 0; k < 3; ++k) {
-        c->send[k].release();
-        c->recv[k].release();
+    for (int s = 0; s < 2; ++s) {
+        for (int k = 0; k < 3; ++k) {
+            c->send[s][k].release();
+            c->recv[s][k].release();
+        }
+        if (c->rendered[s]) (void)hipEventDestroy(c->rendered[s]);
+        if (c->freed[s]) (void)hipEventDestroy(c->freed[s]);
     }
+    if (c->gstream) (void)hipStreamDestroy(c->gstream);
     delete c;
+    return RT_OK;
+}
+
+rt_status rt_comm_synchronize(rt_comm* c) {
+    if (!c) return fail(RT_ERR_INVALID_ARG, "comm is NULL");
+    DeviceGuard g(c->device);
+    RT_HIP(hipStreamSynchronize(c->ctx->stream));
+    RT_HIP(hipStreamSynchronize(c->gstream));
     return RT_OK;
 }
 
@@ -521,15 +597,14 @@ rt_status rt_render_gather(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
     if (st == RT_OK) st = check_root_outputs(c, outputs, dst);
     if (st != RT_OK) return st;
     DeviceGuard g(c->device);
-    Plan pl;
-    rt_comm::Ev* ev = nullptr;
-    st = render_part(c, sc, cam, opts, outputs, pl, ev);
+    Frame f;
+    st = render_part(c, sc, cam, opts, outputs, f);
     if (st != RT_OK) return st;
     RT_NCCL(ncclGroupStart());
-    st = gather_part(c, cam, outputs, pl);
+    st = gather_part(c, cam, outputs, f);
     RT_NCCL(ncclGroupEnd());
     if (st != RT_OK) return st;
-    return assemble_part(c, cam, outputs, pl, dst, ev);
+    return assemble_part(c, cam, outputs, f, dst);
 }
 
 rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, int n,
@@ -546,23 +621,22 @@ rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, i
     void* const dst[3] = {d_hdr64, d_hdr32, d_ldr};
     st = check_root_outputs(comms[0], outputs, dst);
     if (st != RT_OK) return st;
-    std::vector<Plan> pl(static_cast<size_t>(n));
-    std::vector<rt_comm::Ev*> ev(static_cast<size_t>(n), nullptr);
+    std::vector<Frame> f(static_cast<size_t>(n));
     for (int i = 0; i < n; ++i) {  // 1. every GPU renders its rows (asynchronous)
         DeviceGuard g(comms[i]->device);
-        st = render_part(comms[i], scenes[i], cam, opts, outputs, pl[i], ev[i]);
+        st = render_part(comms[i], scenes[i], cam, opts, outputs, f[i]);
         if (st != RT_OK) return st;
     }
     RT_NCCL(ncclGroupStart());  // 2. one gather per output over all GPUs
     for (int i = 0; i < n && st == RT_OK; ++i) {
         DeviceGuard g(comms[i]->device);
-        st = gather_part(comms[i], cam, outputs, pl[i]);
+        st = gather_part(comms[i], cam, outputs, f[i]);
     }
     RT_NCCL(ncclGroupEnd());
     if (st != RT_OK) return st;
     for (int i = 0; i < n; ++i) {  // 3. rank 0 assembles; the others close their events
         DeviceGuard g(comms[i]->device);
-        st = assemble_part(comms[i], cam, outputs, pl[i], dst, ev[i]);
+        st = assemble_part(comms[i], cam, outputs, f[i], dst);
         if (st != RT_OK) return st;
     }
     return RT_OK;

@@ -146,3 +146,37 @@ def test_assemble_rows_matches_row_planner(ctx, n, block, H, row_bytes):
             k += b - a
     out = ctx.debug_assemble_rows(gathered, H, block, n, max_rows)
     assert np.array_equal(out, image)
+
+
+def test_render_gather_pipelined_frames(ctx, comm1):
+    """RT_FLAG_PIPELINE: frame k's gather + assembly run on the communicator's stream while frame
+    k+1 renders (two slots).  Five frames from five cameras into five framebuffers, enqueued back
+    to back, each equal to its own rt_render; then a serial frame after them."""
+    sc = make_config("c3", 640, 360)
+    W, H = 640, 360
+    ds = ctx.scene(sc)
+    try:
+        base = ds.camera["position"][0].copy()
+        cams = [base + (0.5 * k, -0.25 * k, 0.0) for k in range(5)]
+        refs = []
+        for cpos in cams:
+            ds.camera["position"][0] = cpos
+            refs.append(ds.render(hdr64=False, tonemap=1)["ldr"])
+        outs = [torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda") for _ in cams]
+        flags = capi.RT_FLAG_PIPELINE | capi.RT_FLAG_TIME_KERNEL
+        for cpos, o in zip(cams, outs):
+            ds.camera["position"][0] = cpos
+            comm1.render_gather(ds, capi.default_opts(tonemap=1, flags=flags), capi.RT_OUT_LDR,
+                                None, None, o.data_ptr())
+        serial = torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda")
+        comm1.render_gather(ds, capi.default_opts(tonemap=1), capi.RT_OUT_LDR, None, None,
+                            serial.data_ptr())
+        comm1.synchronize()
+        for k, (o, ref) in enumerate(zip(outs, refs)):
+            assert np.array_equal(o.cpu().numpy().reshape(H, W, 3), ref), k
+        assert np.array_equal(serial.cpu().numpy().reshape(H, W, 3), refs[-1])
+        ds.camera["position"][0] = base
+    finally:
+        ds.close()
+    t = comm1.timing(reset=True)
+    assert t.frames == 5 and t.render_ms > 0 and t.assemble_ms > 0
