@@ -298,8 +298,9 @@ rt_status rt_intersect_rays(rt_context* ctx, const rt_scene* scene, const double
 rt_status rt_tonemap(rt_context* ctx, const double* hdr, size_t n_pixels, int op,
                      uint8_t* ldr_out);
 
-/* Test hook: evaluates x/y, sqrt(x), pow(x,y), log(x) on the device for n inputs so the
- * parity suite can pin device libm against the host's.  out: 4*n doubles. */
+/* Test hook: evaluates x/y, sqrt(x), pow(x,y), log(x) and the Blinn-Phong pow of the trace
+ * kernels (rt_device.hpp pow_bp) on the device for n inputs so the parity suite can pin device
+ * libm against the host's.  out: 5*n doubles. */
 rt_status rt_debug_f64_ops(rt_context* ctx, const double* x, const double* y, size_t n,
                            double* out);
 

@@ -46,15 +46,18 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
     # the recipe itself is a dependency: a change of HIP_FLAGS / EXTRA_FLAGS / SOURCES rebuilds.
     # Objects are rebuilt per source: a source's object is stale when the source, any header
     # (csrc/*.hpp, include/rt_capi.h) or this recipe is newer.
-    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))] + [
-        os.path.join(ROOT, "include", "rt_capi.h"), os.path.abspath(__file__)]
+    # (.hip sources also depend on the other .hip files: rt_trace_lean.hip includes rt_trace.hip)
+    common = [os.path.join(ROOT, "include", "rt_capi.h"), os.path.abspath(__file__)]
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    hip_files = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip")]
     os.makedirs(OBJ_DIR, exist_ok=True)
     inc = f"-I{os.path.join(ROOT, 'include')}"
     procs, objs = [], []
     for src in SOURCES:  # one hipcc per stale source, in parallel
         obj = os.path.join(OBJ_DIR, src + ".o")
         objs.append(obj)
-        if not force and not _stale(obj, [os.path.join(CSRC, src)] + headers):
+        deps = [os.path.join(CSRC, src)] + headers + common + (hip_files if src.endswith(".hip") else [])
+        if not force and not _stale(obj, deps):
             continue
         cmd = [HIPCC, *HIP_FLAGS, *EXTRA_FLAGS.get(src, []), inc, "-c", "-o", obj,
                os.path.join(CSRC, src)]

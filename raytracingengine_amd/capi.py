@@ -232,7 +232,7 @@ class Context:
     def debug_f64_ops(self, x: np.ndarray, y: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, np.float64)
         y = np.ascontiguousarray(y, np.float64)
-        out = np.empty((x.size, 4), np.float64)
+        out = np.empty((x.size, 5), np.float64)
         _check(_lib.rt_debug_f64_ops(self._h, x.ctypes.data, y.ctypes.data, x.size,
                                      out.ctypes.data))
         return out

@@ -749,14 +749,14 @@ rt_status rt_debug_f64_ops(rt_context* ctx, const double* x, const double* y, si
                            double* out) {
     if (!ctx || !x || !y || !out) return fail(RT_ERR_INVALID_ARG, "NULL argument");
     DeviceGuard g(ctx->device);
-    RT_HIP(ctx->dbg.ensure(n * 6 * sizeof(double)));
+    RT_HIP(ctx->dbg.ensure(n * 7 * sizeof(double)));
     double* dx = static_cast<double*>(ctx->dbg.ptr);
     double* dy = dx + n;
     double* dout = dy + n;
     RT_HIP(hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     RT_HIP(hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     RT_HIP(launch_debug_f64(dx, dy, n, dout, ctx->stream));
-    RT_HIP(hipMemcpyAsync(out, dout, 4 * n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(hipMemcpyAsync(out, dout, 5 * n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(hipStreamSynchronize(ctx->stream));
     return RT_OK;
 }

@@ -703,7 +703,7 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
             const d3 H = unit(L + view);
             const double ndh = smax(0.0, dot(n, H));
             if (ndh > 0.0) {
-                const double sf = pow(ndh, m[3]);
+                const double sf = pow_bp(ndh, m[3]);
                 spec = spec + ((E * inv_d2) * sf) * T;
             }
         }

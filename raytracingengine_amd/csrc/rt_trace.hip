@@ -24,13 +24,13 @@ namespace rtamd {
 namespace lean {
 #endif
 
-template <int PATH, bool COUNT, bool LDS, bool LSTK = false>
-__global__ __launch_bounds__(kTileW * kTileH, 2) void trace_kernel(TraceParams P) {
+// MINW: minimum waves per SIMD the register budget is compiled for; SINGLE: one sample per pixel
+// (AA = 1: no sample loop, no accumulator live across the trace).
+template <int PATH, bool COUNT, bool LDS, int MINW = 2, bool SINGLE = false>
+__global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParams P) {
     extern __shared__ double smem[];
     const int tid = threadIdx.y * kTileW + threadIdx.x;
     const SceneView S = stage_scene<LDS>(P, smem, tid, kTileW * kTileH);
-    // chain stack in LDS after the staged scene (scene_doubles() of them when LDS)
-    double* lstk = smem + (LDS ? scene_doubles(P) : 0) + tid;
     const uint32_t x = blockIdx.x * kTileW + threadIdx.x;
     const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
     Counts cnt{0u, 0u};
@@ -49,14 +49,14 @@ __global__ __launch_bounds__(kTileW * kTileH, 2) void trace_kernel(TraceParams P
         // GeneratePixelAt (Scene.h:283-304)
         d3 acc = mk(0.0, 0.0, 0.0);
         int samples = 0;
-        for (int s = 0; s < P.aa; ++s) {
+        const int nsamples = SINGLE ? 1 : P.aa;
+        for (int s = 0; s < nsamples; ++s) {
             const d3 dir = camera_dir(P, cam, x, y, pix, s);
             d3 c;
             if constexpr (PATH == kPathDirect)
                 c = trace_direct<COUNT>(S, P, cam, dir, pix, static_cast<uint32_t>(s), cnt);
             else if constexpr (PATH == kPathChain)
-                c = trace_chain<COUNT, LSTK>(S, P, cam, dir, pix, static_cast<uint32_t>(s), cnt,
-                                             lstk, kTileW * kTileH);
+                c = trace_chain<COUNT>(S, P, cam, dir, pix, static_cast<uint32_t>(s), cnt);
             else
                 c = trace_tree<COUNT>(S, P, cam, dir, pix, static_cast<uint32_t>(s), cnt);
             acc = acc + c;
@@ -79,43 +79,41 @@ __global__ __launch_bounds__(kTileW * kTileH, 2) void trace_kernel(TraceParams P
     }
 }
 
-// LDS chain stack: 4 doubles (value xyz, weight) per pending level per thread; a chain keeps
-// at most max_recursion - 1 levels pending (the last one folds with the sky at once)
-static size_t chain_stack_bytes(const TraceParams& p) {
-    return sizeof(double) * 4 * static_cast<size_t>(p.max_rec > 1 ? p.max_rec - 1 : 0) *
-           kTileW * kTileH;
-}
-
-template <int PATH, bool COUNT, bool LDS, bool LSTK>
+template <int PATH, bool COUNT, bool LDS, int MINW, bool SINGLE>
 static hipError_t launch_one(const TraceParams& p, size_t lds_bytes, hipStream_t stream) {
     const dim3 block(kTileW, kTileH);
     const dim3 grid((p.width + kTileW - 1) / kTileW, (p.rows + kTileH - 1) / kTileH);
-    const size_t smem = (LDS ? lds_bytes : 0) + (LSTK ? chain_stack_bytes(p) : 0);
-    hipLaunchKernelGGL((trace_kernel<PATH, COUNT, LDS, LSTK>), grid, block, smem, stream, p);
+    hipLaunchKernelGGL((trace_kernel<PATH, COUNT, LDS, MINW, SINGLE>), grid, block,
+                       LDS ? lds_bytes : 0, stream, p);
     return hipGetLastError();
 }
 
-template <int PATH, bool LSTK>
+template <int PATH, int MINW, bool SINGLE>
 static hipError_t launch_lds(const TraceParams& p, bool count, bool lds, size_t lds_bytes,
                              hipStream_t stream) {
     if (count)
-        return lds ? launch_one<PATH, true, true, LSTK>(p, lds_bytes, stream)
-                   : launch_one<PATH, true, false, LSTK>(p, lds_bytes, stream);
-    return lds ? launch_one<PATH, false, true, LSTK>(p, lds_bytes, stream)
-               : launch_one<PATH, false, false, LSTK>(p, lds_bytes, stream);
+        return lds ? launch_one<PATH, true, true, MINW, SINGLE>(p, lds_bytes, stream)
+                   : launch_one<PATH, true, false, MINW, SINGLE>(p, lds_bytes, stream);
+    return lds ? launch_one<PATH, false, true, MINW, SINGLE>(p, lds_bytes, stream)
+               : launch_one<PATH, false, false, MINW, SINGLE>(p, lds_bytes, stream);
 }
 
 template <int PATH>
 static hipError_t launch_path(const TraceParams& p, bool count, bool lds, size_t lds_bytes,
                               hipStream_t stream) {
+#ifdef RT_LEAN_GENERIC
+    // Reflection chains (C1, mirror) without triangles / area light: compiled for 3 waves/SIMD
+    // (168 VGPRs; the forward-accumulated chain needs no stack) — C1 702 -> 568 us, mirror
+    // 2189 -> 1684 us on MI355X; 4 waves spills 320 B/lane and loses (C1 900 us).  AA = 1 takes
+    // the single-sample instantiation (80 instead of 144 B/lane of spills).
     if constexpr (PATH == kPathChain) {
-        // reflection chains keep their pending levels in LDS when two 256-thread workgroups
-        // still fit a CU (the kernel runs at 2 waves/SIMD anyway): max_recursion 10 = 72 KiB
-        const size_t total = (lds ? lds_bytes : 0) + chain_stack_bytes(p);
-        if (p.max_rec > 1 && total <= 80 * 1024)
-            return launch_lds<PATH, true>(p, count, lds, lds_bytes, stream);
+        if (p.aa == 1 && !p.redo) return launch_lds<PATH, 3, true>(p, count, lds, lds_bytes, stream);
+        return launch_lds<PATH, 3, false>(p, count, lds, lds_bytes, stream);
+    } else
+#endif
+    {
+        return launch_lds<PATH, 2, false>(p, count, lds, lds_bytes, stream);
     }
-    return launch_lds<PATH, false>(p, count, lds, lds_bytes, stream);
 }
 
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
@@ -163,7 +161,7 @@ __global__ __launch_bounds__(256) void trace_rays_kernel(TraceParams P, const do
         const d3 d = mk(r[3], r[4], r[5]);
         d3 c;
         if constexpr (PATH == kPathDirect) c = trace_direct<COUNT>(S, P, o, d, i, 0u, cnt);
-        else if constexpr (PATH == kPathChain) c = trace_chain<COUNT, false>(S, P, o, d, i, 0u, cnt);
+        else if constexpr (PATH == kPathChain) c = trace_chain<COUNT>(S, P, o, d, i, 0u, cnt);
         else c = trace_tree<COUNT>(S, P, o, d, i, 0u, cnt);
         out[3 * i + 0] = c.x;
         out[3 * i + 1] = c.y;
@@ -262,10 +260,11 @@ hipError_t launch_tonemap(const double* hdr, size_t n, int op, uint8_t* out, hip
 __global__ void debug_f64_kernel(const double* x, const double* y, size_t n, double* out) {
     const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    out[4 * i + 0] = x[i] / y[i];
-    out[4 * i + 1] = sqrt(x[i]);
-    out[4 * i + 2] = pow(x[i], y[i]);
-    out[4 * i + 3] = log(x[i]);
+    out[5 * i + 0] = x[i] / y[i];
+    out[5 * i + 1] = sqrt(x[i]);
+    out[5 * i + 2] = pow(x[i], y[i]);
+    out[5 * i + 3] = log(x[i]);
+    out[5 * i + 4] = pow_bp(x[i], y[i]);
 }
 
 hipError_t launch_debug_f64(const double* x, const double* y, size_t n, double* out,

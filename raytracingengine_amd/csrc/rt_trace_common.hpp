@@ -434,7 +434,7 @@ __device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 vi
         const d3 H = unit(L + view);
         const double ndh = smax(0.0, dot(n, H));
         if (ndh > 0.0) {
-            const double sf = pow(ndh, m.shininess);
+            const double sf = pow_bp(ndh, m.shininess);
             spec = spec + ((E * inv_d2) * sf) * T;
         }
     }
@@ -550,57 +550,28 @@ __device__ __forceinline__ d3 trace_direct(const SceneView& S, const TraceParams
     return shade<false, COUNT>(S, P, o, d, pix, sample, 0, cnt).value;
 }
 
-// TraceRay for opaque scenes: a linear reflection chain.  Levels are pushed front-to-back and
-// folded back-to-front, final_k = value_k + child_k * rw_k, the reference's rounding order.
-// The chain's pending levels (value, weight) live either in private memory (scratch) or, when
-// the workgroup has room, in LDS: `lstk` points at this thread's column of a structure-of-arrays
-// block [level][component][thread] with `stride` = threads per workgroup (conflict-free).
-template <bool COUNT, bool LSTK>
+// TraceRay for opaque scenes: a linear reflection chain (Scene.h:131-198 with transparency 0).
+// The reference folds it back to front, final_k = value_k + final_{k+1}·rw_k; here it is
+// accumulated front to back, acc += W_k·value_k with W_{k+1} = W_k·rw_k, so no level has to wait
+// on a stack (the kernel holds four doubles of chain state instead of 4·(max_recursion − 1)).
+// Same sum, different rounding order: a relative difference of a few ε per level (every chain
+// scene already calls libm pow, so these are held to 1e-12, not to bit equality).
+template <bool COUNT>
 __device__ __forceinline__ d3 trace_chain(const SceneView& S, const TraceParams& P, d3 o, d3 d,
-                                          uint64_t pix, uint32_t sample, Counts& cnt,
-                                          double* lstk = nullptr, int stride = 0) {
-    d3 base[LSTK ? 1 : kMaxDepth];
-    double w[LSTK ? 1 : kMaxDepth];
-    int depth = 0;
-    d3 leaf;
-    while (true) {
-        if (depth >= P.max_rec) {
-            leaf = sky(d);
+                                          uint64_t pix, uint32_t sample, Counts& cnt) {
+    d3 acc = mk(0.0, 0.0, 0.0);
+    double w = 1.0;
+    for (int depth = 0;; ++depth) {
+        if (depth >= P.max_rec) {  // TraceRay at depth maxRecursion: the sky (Scene.h:132-134)
+            acc = acc + sky(d) * w;
             break;
         }
         const Node nd = shade<false, COUNT>(S, P, o, d, pix, sample, depth, cnt);
-        if (!nd.hit || !nd.refl) {
-            leaf = nd.value;
-            break;
-        }
-        if (depth + 1 >= P.max_rec) {
-            // the child is TraceRay at depth maxRecursion: the sky (Scene.h:132-134); fold
-            // this level right away (the same two operations the stack would do)
-            leaf = nd.value + sky(nd.rd) * nd.rw;
-            break;
-        }
-        if constexpr (LSTK) {
-            double* f = lstk + 4 * depth * stride;
-            f[0] = nd.value.x;
-            f[stride] = nd.value.y;
-            f[2 * stride] = nd.value.z;
-            f[3 * stride] = nd.rw;
-        } else {
-            base[depth] = nd.value;
-            w[depth] = nd.rw;
-        }
+        acc = acc + nd.value * w;
+        if (!nd.hit || !nd.refl) break;
+        w = w * nd.rw;
         o = nd.ro;
         d = nd.rd;
-        ++depth;
-    }
-    d3 acc = leaf;
-    for (int k = depth - 1; k >= 0; --k) {
-        if constexpr (LSTK) {
-            const double* f = lstk + 4 * k * stride;
-            acc = mk(f[0], f[stride], f[2 * stride]) + acc * f[3 * stride];
-        } else {
-            acc = base[k] + acc * w[k];
-        }
     }
     return acc;
 }

@@ -49,6 +49,27 @@ def test_device_libm(ctx):
     assert np.all(np.abs(out[:, 3] - lg) <= np.spacing(np.abs(lg)))
 
 
+def test_blinn_phong_pow_accuracy(ctx):
+    """pow_bp (rt_device.hpp), the Blinn-Phong pow(N·H, shininess) of every trace kernel: within
+    2.5e-16 absolute of libm pow on (0, 1] x [0, 4096] (results in [0, 1]), and the libm value
+    itself outside its fast domain."""
+    rng = np.random.default_rng(5)
+    n = 200000
+    x = np.concatenate([rng.uniform(0, 1, n), np.exp2(rng.uniform(-1074, 0, n)),
+                        1.0 - rng.uniform(0, 1e-6, n), [1.0, 1.0 + 2 ** -52, 5e-324, 0.5]])
+    y = np.concatenate([rng.uniform(0, 300, n), rng.uniform(0, 4096, n), rng.uniform(0, 1, n),
+                        [0.128, 128.0, 0.5, 0.0]])
+    y[::7] = 0.128  # the reference scene's shininess
+    out = ctx.debug_f64_ops(x, y)
+    with np.errstate(all="ignore"):
+        ref = np.power(x, y)
+    assert np.all(np.abs(out[:, 4] - ref) <= 2.5e-16), np.abs(out[:, 4] - ref).max()
+    odd_x = np.array([2.0, 0.0, -0.5, np.inf, np.nan, 0.3, 0.3, 0.3])
+    odd_y = np.array([3.0, 2.0, 2.0, 1.0, 1.0, np.nan, np.inf, -1e300])
+    odd = ctx.debug_f64_ops(odd_x, odd_y)
+    assert _same_bits(odd[:, 4], odd[:, 2])  # out of its domain: the libm pow
+
+
 def _same_bits(a, b):
     """Bitwise equality (signed zeros distinguished), any NaN equal to any NaN."""
     nan = np.isnan(a) & np.isnan(b)
@@ -549,8 +570,10 @@ def test_render_device_into_torch_buffers(ctx):
                                              ("glass", 3, 6), ("mesh", 1, 10), ("glass", 1, 16)])
 def test_wavefront_equals_per_pixel_kernel(ctx, monkeypatch, name, aa, max_rec):
     """Scenes with secondary rays render level by level (rt_wavefront.hip); the image must be
-    bit-identical to the per-pixel DFS kernel (RT_FLAG_GENERIC_KERNEL) — same rays, same fold
-    order — for the chain (mirror, c1) and the tree (glass) shapes, with AA and deep recursion."""
+    bit-identical to the per-pixel DFS kernel (RT_FLAG_GENERIC_KERNEL) for the tree (glass)
+    shape — same rays, same fold order — with AA and deep recursion.  Reflection chains (mirror,
+    c1, mesh) are folded back to front breadth-first but accumulated front to back per pixel
+    (rt_trace_common.hpp trace_chain): the same sums in another rounding order, within 1e-12."""
     sc = make_config(name, 160, 90, aa=aa)
     monkeypatch.setenv("RTAMD_WF_CHAIN", "1")  # chains are per-pixel by default
     ds = ctx.scene(sc)
@@ -560,8 +583,13 @@ def test_wavefront_equals_per_pixel_kernel(ctx, monkeypatch, name, aa, max_rec):
                       flags=capi.RT_FLAG_GENERIC_KERNEL)
     finally:
         ds.close()
-    assert np.array_equal(a["hdr64"], b["hdr64"], equal_nan=True)
-    assert np.array_equal(a["ldr"], b["ldr"])
+    if name == "glass":
+        assert np.array_equal(a["hdr64"], b["hdr64"], equal_nan=True)
+        assert np.array_equal(a["ldr"], b["ldr"])
+    else:
+        assert np.abs(a["hdr64"] - b["hdr64"]).max() <= POW_TOL
+        same = np.all(a["hdr64"] == b["hdr64"], axis=-1)
+        assert np.array_equal(a["ldr"][same], b["ldr"][same])
 
 
 @pytest.mark.parametrize("mb", ["1", "2"])

@@ -1,7 +1,8 @@
 """Register budgets of the built gfx950 kernels (CPU: reads the code objects' metadata).
 
 Occupancy is the lever measured most in DESIGN.md §4: the single-sample packet kernels run at
-5 waves/SIMD (≤ 96 VGPRs + AGPRs) and the generic / breadth-first trace kernels at 2 (≤ 256).
+5 waves/SIMD (≤ 96 VGPRs + AGPRs), the lean reflection-chain kernels at 3 (≤ 168: C1 -19 %,
+mirror -23 % against 2) and the other generic / breadth-first trace kernels at 2 (≤ 256).
 An unrelated change once pushed the breadth-first level kernel into AGPRs and 1 wave/SIMD
 (glass +35 %); this pins the budgets on the objects `build()` produced."""
 import os
@@ -59,3 +60,11 @@ def test_generic_trace_kernels_run_at_2_waves(src):
     heavy = {n: r for n, r in ks.items() if "trace_kernel" in n or "wf_level_kernel" in n}
     assert heavy
     assert all(_waves(r) >= 2 for r in heavy.values()), heavy
+
+
+def test_lean_chain_kernels_run_at_3_waves():
+    """trace_kernel<PATH = chain, COUNT, LDS, MINW = 3, SINGLE> of rt_trace_lean.hip (C1, mirror)."""
+    ks = _kernels("rt_trace_lean.hip")
+    chain = {n: r for n, r in ks.items() if re.search(r"trace_kernelILi1ELb[01]ELb[01]ELi3E", n)}
+    assert len(chain) == 8, sorted(ks)
+    assert all(_waves(r) >= 3 for r in chain.values()), chain

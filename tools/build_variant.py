@@ -12,6 +12,11 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from raytracingengine_amd import build as B
 
 args = sys.argv[1:]
+srcs = None  # --src a.hip,b.hip: the sources to recompile (when FILE is a header)
+if "--src" in args:
+    i = args.index("--src")
+    srcs = args[i + 1].split(",")
+    del args[i:i + 2]
 defs = []
 while "-D" in args:
     i = args.index("-D")
@@ -29,14 +34,17 @@ for old, new in zip(reps[::2], reps[1::2]):
     assert old in text, f"patch text not found: {old[:60]!r}"
     text = text.replace(old, new)
 open(path, "w").write(text)
-obj = os.path.join(tmp, fname + ".o")
 inc = f"-I{os.path.join(B.ROOT, 'include')}"
-subprocess.check_call([B.HIPCC, *B.HIP_FLAGS, *B.EXTRA_FLAGS.get(fname, []), *defs, inc, "-c",
-                       "-o", obj, path], stderr=subprocess.DEVNULL)
-objs = [obj if s == fname else os.path.join(B.OBJ_DIR, s + ".o") for s in B.SOURCES]
+rebuilt = {}
+for src in srcs or [fname]:
+    obj = os.path.join(tmp, src + ".o")
+    subprocess.check_call([B.HIPCC, *B.HIP_FLAGS, *B.EXTRA_FLAGS.get(src, []), *defs, inc, "-c",
+                           "-o", obj, os.path.join(src_dir, src)], stderr=subprocess.DEVNULL)
+    rebuilt[src] = obj
+objs = [rebuilt.get(s, os.path.join(B.OBJ_DIR, s + ".o")) for s in B.SOURCES]
 out_dir = os.path.join(B.ROOT, "tools", "variants")
 os.makedirs(out_dir, exist_ok=True)
 out = os.path.join(out_dir, name + ".so")
-subprocess.check_call([B.HIPCC, *B.HIP_FLAGS, "-shared", "-o", out, *objs])
+subprocess.check_call([B.HIPCC, *B.HIP_FLAGS, "-shared", "-o", out, *objs, *B.LINK_LIBS])
 shutil.rmtree(tmp)
 print(out)
