@@ -34,13 +34,13 @@ std::vector<Color> tonemapOp(const std::vector<Vec3>& pixels, int op, int device
 }
 
 std::vector<Color> tonemap(const std::vector<Vec3>& pixels) {
-    return tonemapOp(pixels, RT_TONEMAP_ACES);
+    return tonemapOp(pixels, RT_TONEMAP_ACES, current_device());
 }
 
 std::vector<std::vector<Color>> tonemapAll(const std::vector<Vec3> pixels) {
     std::vector<Color> planes(pixels.size() * RT_TONEMAP_COUNT);
-    check(rt_tonemap(thread_context(0), reinterpret_cast<const double*>(pixels.data()),
-                     pixels.size(), RT_TONEMAP_COUNT, reinterpret_cast<uint8_t*>(planes.data())),
+    check(rt_tonemap(thread_context(current_device()),
+                     reinterpret_cast<const double*>(pixels.data()), pixels.size(), RT_TONEMAP_COUNT, reinterpret_cast<uint8_t*>(planes.data())),
           "rt_tonemap");
     std::vector<std::vector<Color>> all(RT_TONEMAP_COUNT);
     for (int k = 0; k < RT_TONEMAP_COUNT; ++k)

@@ -19,6 +19,7 @@ void writePPM(const std::string& filename, const std::vector<Color>& pixels, siz
 
 namespace rtamd {
 // One operator (rt_tonemap_op) followed by toColor(), evaluated on the GPU.
+// tonemap() and tonemapAll() run on rtamd::current_device() (scene.hpp).
 std::vector<Color> tonemapOp(const std::vector<Vec3>& pixels, int op, int device = 0);
 // tonemap(): ACES (RaytracingEngine.cpp:165-174).
 std::vector<Color> tonemap(const std::vector<Vec3>& pixels);

@@ -20,6 +20,7 @@ struct ThreadContexts {
     }
 };
 thread_local ThreadContexts t_contexts;
+thread_local int t_device = 0;  // the device this thread's last Scene render ran on
 
 void put3(double* d, const Vec3& v) {
     d[0] = v.x;
@@ -36,6 +37,8 @@ rt_material material_desc(const Material& m) {
     return o;
 }
 }  // namespace
+
+int current_device() { return t_device; }
 
 rt_context* thread_context(int device) {
     auto it = t_contexts.by_device.find(device);
@@ -88,6 +91,7 @@ rt_render_opts Scene::optsDesc(int tonemap) const {
 }
 
 rt_scene* Scene::upload() const {
+    rtamd::t_device = device_;
     if (dev_ && dev_->version == version_ && dev_->device == device_) return dev_->scene;
     dev_ = uploadTo(device_);
     return dev_->scene;

@@ -28,6 +28,9 @@ struct SceneDevice;  // uploaded copy of a Scene on one device (scene.cpp)
 
 // The calling thread's context for `device` (created on first use, one per thread+device).
 rt_context* thread_context(int device);
+// The device of this thread's last single-GPU Scene call (Scene::SetDevice; 0 before any):
+// tonemap() / tonemapAll() run there, next to the frame they usually follow.
+int current_device();
 // Throws std::runtime_error carrying rt_last_error() when st != RT_OK.
 void check(rt_status st, const char* what);
 }  // namespace rtamd

@@ -544,7 +544,10 @@ rt_status rt_scene_create(rt_context* ctx, const rt_scene_desc* d, rt_scene** ou
 rt_status rt_scene_destroy(rt_scene* sc) {
     if (!sc) return RT_OK;
     DeviceGuard g(sc->ctx->device);
-    (void)hipStreamSynchronize(sc->ctx->stream);
+    // Launches that read the scene or its packet images may be in flight on any stream the
+    // context used (rt_context_set_stream switches it; pipelined frames use several), not only
+    // the current one: wait for the whole device before freeing.
+    (void)hipDeviceSynchronize();
     sc->buf.release();
     for (auto& im : sc->pk_images) {
         im.buf.release();

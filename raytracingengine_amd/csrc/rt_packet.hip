@@ -46,6 +46,16 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr double kCullRel = 1e-4;   // relative inflation of every culling radius
 constexpr double kFarRatio = 1e5;   // |oc|/r beyond which a sphere is never culled
 constexpr double kNoWin = 1.0 + 0x1.0p-40;  // "quotient provably >= best" factor
+// Point-light shadow packets with more candidate spheres than this are split in two (pk_light);
+// variants with more than 64 spheres only (MAXC > 1).
+#ifndef RT_SHADOW_SPLIT
+#define RT_SHADOW_SPLIT 1
+#endif
+#ifndef RT_SHADOW_SPLIT_MIN
+#define RT_SHADOW_SPLIT_MIN 16
+#endif
+constexpr bool kShadowSplit = RT_SHADOW_SPLIT != 0;
+constexpr int kShadowSplitMin = RT_SHADOW_SPLIT_MIN;
 
 // Feature bits of a kernel variant: code for a feature the scene does not use is not compiled
 // in, which is what keeps the FP64 register budget (and so the occupancy) down.
@@ -689,12 +699,95 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     const d3 so = P + n * bias;
     const uint64_t casting = __ballot(need);
     if (!casting) return;  // no lane casts this shadow ray (uniform)
-    const Masks<MAXC> M = pre ? *pre : shadow_masks<MAXC, FEAT>(S, need, so, lcenter, lrad, bias);
+    // every lane stays in the code below until the march mask is formed (wave reductions);
+    // lanes that cast no ray only take part in them
+    int occ = 0;
+    Masks<MAXC> M;
+    if (pre) {
+        M = *pre;
+        if (need) occ = pk_occlusion<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
+    } else {
+        const OriginBall B = origin_ball(need, so);
+        M = B.ok ? cull_capsule<MAXC, FEAT>(S, B.c, B.R, lcenter, lrad, bias)
+                 : all_candidates<MAXC>(S.ns);
+        bool split = false;
+        if constexpr (kShadowSplit && MAXC > 1) {
+            // A wide packet (origins straddling a depth edge: a sphere in front of a wall) gets a
+            // fat capsule that keeps much of the scene, and every lane then classifies every
+            // candidate: these waves run 10-35x the median and set the tail of a launch.  Such
+            // a packet is split in two — the lanes within R/2 of the ball's centre and the rest —
+            // each with its own ball and capsule (ANDed with the shared mask), and each group
+            // walks only its own candidates.  Masks only shrink by provable misses, so every
+            // lane's classification is unchanged.  The groups' capsules skip the plane cull
+            // (they keep the shared one's plane mask: C3 -0.7 %).  8-rank row splits: slowest
+            // rank C4 0.30 → 0.20 ms, C3 0.11 → 0.09 ms (with the march mask below); one whole
+            // frame: C4 -1 %, C3 +1.2 %, C2/C5 ±0.5 % (tools/gpu_ab.sh, 3 interleaved rounds).
+            int cand = 0;
+#pragma unroll
+            for (int c = 0; c < MAXC; ++c) cand += __builtin_popcountll(M.m[c]);
+            split = B.ok && cand > kShadowSplitMin;  // uniform
+            if (split) {
+                float r_lane = 0.0f;
+                if (need) {
+                    const float dx = static_cast<float>(so.x - B.c.x),
+                                dy = static_cast<float>(so.y - B.c.y),
+                                dz = static_cast<float>(so.z - B.c.z);
+                    r_lane = sqrt_f32(dot3f(dx, dy, dz, dx, dy, dz));
+                }
+                const bool near = r_lane <= 0.5f * B.R;
+                Masks<MAXC> Mn = M, Mf = M;
+                const OriginBall Bn = origin_ball(need && near, so);
+                const OriginBall Bf = origin_ball(need && !near, so);
+                if (Bn.ok) {
+                    const Masks<MAXC> t =
+                        cull_capsule<MAXC, (FEAT & ~kFeatPlanes)>(S, Bn.c, Bn.R, lcenter, lrad, bias);
+#pragma unroll
+                    for (int c = 0; c < MAXC; ++c) Mn.m[c] &= t.m[c];
+                    Mn.pm &= t.pm;
+                }
+                if (Bf.ok) {
+                    const Masks<MAXC> t =
+                        cull_capsule<MAXC, (FEAT & ~kFeatPlanes)>(S, Bf.c, Bf.R, lcenter, lrad, bias);
+#pragma unroll
+                    for (int c = 0; c < MAXC; ++c) Mf.m[c] &= t.m[c];
+                    Mf.pm &= t.pm;
+                }
+#pragma unroll 1
+                for (int g = 0; g < 2; ++g) {  // uniform: one group after the other
+                    Masks<MAXC> Mg;
+#pragma unroll
+                    for (int c = 0; c < MAXC; ++c) Mg.m[c] = g == 0 ? Mn.m[c] : Mf.m[c];
+                    Mg.pm = g == 0 ? Mn.pm : Mf.pm;
+                    if (need && near == (g == 0))
+                        occ = pk_occlusion<MAXC, FEAT>(S, Mg, nchunks, so, L, dist - bias, bias);
+                }
+            }
+        }
+        if (!split && need) occ = pk_occlusion<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
+    }
+    // The exact march (computeTransmittance) for the undecided lanes: a handful of lanes whose
+    // shadow ray starts on or next to a surface, marching up to 64 closest-hit steps.  Over the
+    // whole packet's mask such a march visits every candidate of a wide capsule at every step
+    // (the slowest waves of C3 spend > 90 % of their time here), so it gets a capsule of its
+    // own around the marching lanes' origins: every origin of the march lies on the segment
+    // from its shadow-ray origin towards the light, inside that capsule, so the mask still
+    // holds every sphere the march can hit.  C3's slowest waves 240 → 85 µs; its 8-rank
+    // row split went from 1.37-1.45× the mean rank to 1.02-1.04× (profiles/r02_*).
+    const bool undecided = need && occ == 2;
+    double T = occ == 1 ? 0.0 : 1.0;
+    if (__ballot(undecided)) {  // uniform
+        Masks<MAXC> Mu = M;
+        const OriginBall Bu = origin_ball(undecided, so);
+        if (Bu.ok) {
+            const Masks<MAXC> t = cull_capsule<MAXC, FEAT>(S, Bu.c, Bu.R, lcenter, lrad, bias);
+#pragma unroll
+            for (int c = 0; c < MAXC; ++c) Mu.m[c] &= t.m[c];
+            Mu.pm &= t.pm;
+        }
+        if (undecided) T = pk_transmittance<MAXC, FEAT>(S, Mu, nchunks, so, L, dist - bias, bias);
+    }
     if (!need) return;
     if (COUNT) cnt.shadow++;
-    const int occ = pk_occlusion<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
-    double T = occ == 1 ? 0.0 : 1.0;
-    if (occ == 2) T = pk_transmittance<MAXC, FEAT>(S, M, nchunks, so, L, dist - bias, bias);
     if (T <= bias) return;
     diff = diff + ((E * inv_d2) * ndl) * T;
     if constexpr ((FEAT & kFeatSpec) != 0) {

@@ -113,6 +113,10 @@ def hip_tile_renderer(dscene, rank: int, world: int, block: int = DEFAULT_BLOCK,
 
     def render_rows(ranges: list[tuple[int, int]]) -> torch.Tensor:
         rows = plan_rows(ranges)
+        if rows == 0:  # a rank past the last block (H < world·block): nothing to launch
+            kind = torch.float32 if tonemap is None else torch.uint8
+            out = torch.empty((0, width, 3), dtype=kind, device="cuda")
+            return out if dtype is None or tonemap is not None else out.to(dtype)
         opts = render_opts_for(ranges, rank, world, height, block,
                                tonemap=-1 if tonemap is None else tonemap)
         if tonemap is None:

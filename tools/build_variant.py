@@ -38,8 +38,10 @@ inc = f"-I{os.path.join(B.ROOT, 'include')}"
 rebuilt = {}
 for src in srcs or [fname]:
     obj = os.path.join(tmp, src + ".o")
-    subprocess.check_call([B.HIPCC, *B.HIP_FLAGS, *B.EXTRA_FLAGS.get(src, []), *defs, inc, "-c",
-                           "-o", obj, os.path.join(src_dir, src)], stderr=subprocess.DEVNULL)
+    r = subprocess.run([B.HIPCC, *B.HIP_FLAGS, *B.EXTRA_FLAGS.get(src, []), *defs, inc, "-c",
+                        "-o", obj, os.path.join(src_dir, src)], stderr=subprocess.PIPE, text=True)
+    if r.returncode:  # the errors only (the warnings of these sources are known)
+        sys.exit("\n".join(l for l in r.stderr.splitlines() if "error" in l) or r.stderr[-4000:])
     rebuilt[src] = obj
 objs = [rebuilt.get(s, os.path.join(B.OBJ_DIR, s + ".o")) for s in B.SOURCES]
 out_dir = os.path.join(B.ROOT, "tools", "variants")
