@@ -11,8 +11,8 @@
 //   RenderImage :311-328 → GeneratePixelAt :283-304 → getRay (Math.h:99-121) → TraceRay :131-198
 //   → IntersectClosest :218-257 (Sphere::Intersect Shape.h:72-98, Plane::Intersect :149-159,
 //     Triangle::Intersect :202-220) → directLightning :79-129 → computeTransmittance :35-77.
-// The recursion of TraceRay becomes an explicit stack: a linear chain (opaque mirrors) folded
-// back-to-front to keep the reference's rounding order, or a DFS stack for the refraction tree.
+// The recursion of TraceRay becomes a linear chain accumulated front to back (opaque mirrors,
+// trace_chain) or a DFS stack for the refraction tree (the reference's order).
 #include "rt_trace_common.hpp"
 
 #pragma clang fp contract(off)
