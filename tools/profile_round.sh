@@ -1,19 +1,23 @@
 #!/bin/bash
-# Dev tool (runs on the GPU box): the profiles committed for a round.
-#   bash tools/profile_round.sh r01_v5
-# -> gpurun_out/<tag>/{bench.json, stats/, pmc/} ; copy the summaries into profiles/.
-set -e
-TAG=$1
-OUT=gpurun_out/$TAG
-mkdir -p $OUT
+# GPU call (dev tool): the profiles of a round.   bash tools/profile_round.sh TAG
+#   * rocprofv3 counter passes (tools/pmc_passes.sh) of the C2 packet kernel, the C3 packet kernel
+#     and the C1 chain kernel, incl. FETCH_SIZE / WRITE_SIZE for the HBM traffic;
+#   * rocprofv3 --kernel-trace --stats of the headline bench command;
+#   * every config's kernel time (tools/time_configs.py) and the 8-rank row-split balance.
+# Summaries are made afterwards with tools/pmc_summary.py / valu_summary.py / traffic_summary.py.
+set -u
 export TMPDIR=/tmp
-timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
-timeout -k 10 300 python bench.py --no-cpu-baseline --inflight 2 > $OUT/bench_pipelined.json 2>> $OUT/bench.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 bench.py --no-cpu-baseline --steps 200 > $OUT/bench_prof.json 2> $OUT/prof.err
-for grp in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc/p_$grp -o pmc -- python3 tools/profile_kernel.py c2 20 > $OUT/pmc_$grp.log 2>&1
+OUT=gpurun_out/${1:-prof}
+mkdir -p $OUT
+for c in c2 c3 c1; do
+  timeout -k 10 500 bash tools/pmc_passes.sh $OUT/pmc_$c $c 10 > $OUT/pmc_$c.log 2>&1 || { tail $OUT/pmc_$c.log; exit 1; }
+  echo "pmc $c done"
 done
-python3 tools/pmc_summary.py $OUT/pmc > /dev/null
-python3 tools/traffic_summary.py $OUT/pmc/summary.json $OUT/pmc_c2_frames.json c2 $((1920*1080*27))
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- \
+  python3 bench.py --no-cpu-baseline --no-extras > $OUT/bench_prof.json 2> $OUT/prof.err || { tail $OUT/prof.err; exit 1; }
 find $OUT/stats -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
-cat $OUT/bench.json
+cat $OUT/bench_prof.json
+timeout -k 10 300 python -u tools/time_configs.py > $OUT/configs.txt 2>&1 || { tail $OUT/configs.txt; exit 1; }
+cat $OUT/configs.txt
+timeout -k 10 300 python -u tools/tile_balance.py 8 0,16 c2 c3 c4 c5 > $OUT/balance.jsonl 2>&1 || { tail $OUT/balance.jsonl; exit 1; }
+grep max_over $OUT/balance.jsonl | sed 's/"ms": \[[^]]*\], //'
