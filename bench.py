@@ -191,6 +191,9 @@ class Runner:
         torch = self.torch
         for i in range(warmup):
             step(i, False)
+        # drain this rank's work (its RCCL gathers included) before the process group's own
+        # collective: two communicators' kernels are never in flight together
+        torch.cuda.synchronize()
         self.barrier()
         torch.cuda.synchronize()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

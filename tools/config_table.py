@@ -19,7 +19,10 @@ def config(name, w=None, h=None):
     if name == "c1_aa32":
         return make_config("c1", w, h, aa=32) if w else make_config("c1", aa=32)
     return make_config(name, w, h) if w else make_config(name)
-threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+# the cores this process may run on (capped by OMP_NUM_THREADS), one bound thread per core
+threads = len(os.sched_getaffinity(0))
+if int(os.environ.get("OMP_NUM_THREADS", "0") or 0) > 0:
+    threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
 ctx = capi.Context(0)
 s = torch.cuda.Stream(); ctx.set_stream(s.cuda_stream)
 rows = []
@@ -52,7 +55,8 @@ for name in names:
         b = dss.render(hdr64=False, stats=True)
         dss.close()
         srays = b["trace_rays"] + b["shadow_rays"]
-        _, ms, used = po.ref_render(small, repeat=3, threads=threads, want_image=False)
+        _, ms, used = po.ref_render(small, repeat=3, threads=threads, want_image=False,
+                                    bind=True)
         med = sorted(ms)[len(ms) // 2]
         row.update({"cpu_sample": f"same scene at {W // k}x{H // k}, 3 frames, median",
                     "cpu_threads": used, "cpu_ms_per_sample_frame": round(med, 2),
