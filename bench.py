@@ -14,15 +14,19 @@ Contract (driver):  python bench.py --gpus N --steps K --warmup W
     them to rank 0, and rank 0 assembles the frame in image order in its device framebuffer.
     Strong scaling; the per-rank render / gather / assembly times are in the line, and the
     weak-scaling C2 frames throughput is an extra field (`weak_frames`).
-  * W untimed steps, then exactly K timed steps bracketed by barrier + synchronize on both
-    sides; the max over ranks is the time; rank 0 prints ONE JSON line.
+  * Untimed steps for --clock-warmup-ms (default 50 ms) of wall time so the GPU is at its
+    sustained clock (it needs ~30 ms of load to leave idle: 143 → 45 µs per C2 frame,
+    tools/clock_ramp.py), then W untimed steps, then exactly K timed steps bracketed by
+    barrier + synchronize on both sides; the max over ranks is the time; rank 0 prints ONE
+    JSON line.
 
 Extra fields (N=1): `roofline` (HBM-write bound of the trace kernel from live per-launch HIP
 events; traffic and VALU counters from the committed PMC summaries), `roofline_f32` (the same
 launch with the north star's float3 framebuffer), `moving_camera` (a new camera position every
 frame: no cached per-camera packet image), `d2h` (frames/s of the synchronous host-buffer
 render, the drop-in RenderImage()'s path, pageable and pinned), `tiled_1gpu` (the N>1 default
-workload on one GPU through the same gather path: the strong-scaling anchor), `cpu_baseline`
+workload on one GPU through the same gather path: the strong-scaling anchor), `pipelined` (the
+same frames through the C-ABI serving queue rt_queue, 2 in flight), `cpu_baseline`
 (the unmodified reference renderer, oracle/_ref, timed on this host's cores).
 """
 from __future__ import annotations
@@ -62,11 +66,14 @@ def parse_args(argv=None):
                          "gather with frame k+1's render)")
     ap.add_argument("--hdr", choices=["f64", "f32"], default="f64",
                     help="frames mode HDR framebuffer: f64 = the reference's std::vector<Vec3>")
+    ap.add_argument("--clock-warmup-ms", type=float, default=50.0,
+                    help="untimed steps for this much wall time before the W warmup steps, so "
+                         "that the K timed steps run at the GPU's sustained clock")
     ap.add_argument("--event-every", type=int, default=10,
                     help="bracket every n-th timed step with HIP events (0: none)")
-    ap.add_argument("--inflight", type=int, default=1,
-                    help="> 1: also measure K frames with this many in flight on as many "
-                         "streams ('pipelined' field)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="> 1: also measure the frames with this many in flight through the "
+                         "C-ABI serving queue, rt_queue ('pipelined' field; N=1 extras)")
     ap.add_argument("--no-extras", action="store_true",
                     help="headline only (no f32 / moving-camera / D2H / tiled / weak fields)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -185,10 +192,22 @@ class Runner:
         self.dist.all_gather(out, t)
         return [[float(x) for x in o] for o in out]
 
-    def timed(self, step, steps, warmup, region_events=True):
-        """W untimed steps, then K timed steps between barrier + synchronize; returns
-        (elapsed seconds max over ranks, HIP-event region ms per step on the launch stream)."""
+    def timed(self, step, steps, warmup, region_events=True, warm_step=None):
+        """Untimed steps for `--clock-warmup-ms` of wall time (the GPU leaves its idle clock
+        only after ~30 ms of sustained load: tools/clock_ramp.py, C2 143 → 54 → 45 µs/frame
+        over the first 30 ms), then W untimed steps, then K timed steps between barrier +
+        synchronize; returns (elapsed seconds max over ranks, HIP-event region ms per step on
+        the launch stream).  `warm_step` (default `step`) is what the clock warm-up runs: it
+        must not be a collective, since each rank warms up for its own wall time."""
         torch = self.torch
+        warm = warm_step or step
+        t_end = time.perf_counter() + self.args.clock_warmup_ms / 1e3
+        k = 0
+        while time.perf_counter() < t_end:
+            for _ in range(16):
+                warm(-1000000 - k, False)
+                k += 1
+            torch.cuda.synchronize()
         for i in range(warmup):
             step(i, False)
         # drain this rank's work (its RCCL gathers included) before the process group's own
@@ -264,24 +283,27 @@ def frames_mode(R: Runner, sc, steps, warmup, hdr="f64", tonemap=1, event_every=
 
 
 def pipelined_frames(R: Runner, sc, steps, warmup, inflight, tonemap=1):
-    """The same K frames with `inflight` frames in flight on as many HIP streams, each with its
-    own framebuffers (a serving setup: one frame's tail overlaps the next one's start)."""
+    """The same K frames through the C-ABI serving queue (rt_queue): `inflight` frames in flight
+    on as many HIP streams, each with its own framebuffers — one frame's launch tail overlaps the
+    next frame's start."""
     torch, capi = R.torch, R.capi
     W, H = sc.camera.width, sc.camera.height
     dscene = R.ctx.scene(sc)
-    streams = [R.stream] + [torch.cuda.Stream() for _ in range(inflight - 1)]
+    q = capi.Queue(R.ctx, inflight)
     bufs = [(torch.empty(H * W * 3, dtype=torch.float64, device="cuda"),
-             torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")) for _ in streams]
+             torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")) for _ in range(inflight)]
     opts = capi.default_opts(tonemap=tonemap)
 
     def step(i, timed):
-        k = i % inflight
-        R.ctx.set_stream(streams[k].cuda_stream)
-        h, l = bufs[k]
-        dscene.render_device(h.data_ptr(), None, l.data_ptr(), opts)
+        # frame i goes to slot i mod depth: the queue's stream order keeps a slot's frames in
+        # order, so its framebuffers are rewritten only after the previous frame wrote them (a
+        # consumer would rt_queue_wait(ticket) before reading; nothing here reads them)
+        h, l = bufs[i % inflight]
+        q.submit(dscene, opts, h.data_ptr(), None, l.data_ptr())
 
     elapsed, _ = R.timed(step, steps, warmup, region_events=False)
-    R.ctx.set_stream(R.stream.cuda_stream)
+    q.synchronize()
+    q.close()
     dscene.close()
     return elapsed
 
@@ -354,8 +376,22 @@ def tiled_mode(R: Runner, sc, steps, warmup, gather="u8", tonemap=1, block=16,
         ev = timed and event_every > 0 and i % event_every == 0
         comm.render_gather(dscene, timed_opts if ev else opts, outputs, *ptrs)
 
+    # the clock warm-up renders this rank's rows without the gather (no collective)
+    wopts = capi.default_opts(tonemap=tm)
+    for f, _ in capi.RenderOpts._fields_:
+        if f.startswith("row_"):
+            setattr(wopts, f, getattr(plan, f))
+    wrows = capi.rendered_rows(wopts, H) if wopts.row_begin < H else 0
+    wbuf = torch.empty(max(wrows, 1) * W * bpp, dtype=torch.uint8, device="cuda")
+    wptrs = [None, None, None]
+    wptrs[{"f64": 0, "f32": 1, "u8": 2}[gather]] = wbuf.data_ptr()
+
+    def warm_step(i, timed):
+        if wrows:
+            dscene.render_device(*wptrs, wopts)
+
     comm.timing(reset=True)
-    elapsed, _ = R.timed(step, steps, warmup, region_events=False)
+    elapsed, _ = R.timed(step, steps, warmup, region_events=False, warm_step=warm_step)
     t = comm.timing(reset=True)
     per = [t.render_ms / max(t.frames, 1), t.gather_ms / max(t.frames, 1),
            t.assemble_ms / max(t.frames, 1), float(t.rows), float(rays_rank)]
@@ -428,6 +464,7 @@ def main(argv=None):
                 "parallelism": f"frames x{R.world}", "rays_per_frame": rays_rank,
             },
             "frames_per_sec": round(frames / elapsed, 3),
+            "clock_warmup_ms": args.clock_warmup_ms,
             "kernel_ms_per_launch": round(kernel_ms, 6),
             "kernel_ms_sampled_events": round(res["sampled_ms"], 6) if res["sampled_ms"] else None,
             "roofline": {
@@ -460,13 +497,14 @@ def main(argv=None):
                 "note": "camera x moved by 1e-7 every frame: the per-camera packet image is "
                         "never reused; rays counted at the first position"}
             if args.inflight > 1:
-                el = pipelined_frames(R, sc, args.steps, args.warmup, args.inflight, tonemap)
+                el = pipelined_frames(R, sc, steps_x, args.warmup, args.inflight, tonemap)
                 line["pipelined"] = {
                     "inflight": args.inflight,
-                    "value": round(rays_rank * args.steps / el / 1e6, 3),
-                    "ms_per_step": round(el / args.steps * 1e3, 5),
-                    "note": "same K frames in flight on several HIP streams (serving "
-                            "throughput); not the headline value"}
+                    "value": round(rays_rank * steps_x / el / 1e6, 3),
+                    "ms_per_step": round(el / steps_x * 1e3, 5),
+                    "note": "the same frames through the C-ABI serving queue (rt_queue), "
+                            "several in flight on separate HIP streams; serving throughput, "
+                            "not the headline value"}
             line["d2h"] = d2h_frames(R, sc, min(args.steps, 20), tonemap)
             # the N>1 default workload (C4 tiled + RCCL gather) on this one GPU
             sc4 = make_config("c4", aa=1)
@@ -508,6 +546,7 @@ def main(argv=None):
                 "rays_per_frame": res["rays"],
             },
             "frames_per_sec": round(args.steps / elapsed, 3),
+            "clock_warmup_ms": args.clock_warmup_ms,
             "tiled": summ,
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

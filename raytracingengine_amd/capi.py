@@ -42,7 +42,8 @@ EXPORTED = [
     "rt_comm_destroy", "rt_comm_info", "rt_render_gather", "rt_render_gather_all",
     "rt_comm_timing", "rt_comm_synchronize", "rt_debug_assemble_rows",
     "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
-    "rt_debug_f64_ops", "rt_debug_vec_ops",
+    "rt_debug_f64_ops", "rt_debug_vec_ops", "rt_queue_create", "rt_queue_destroy",
+    "rt_queue_submit", "rt_queue_wait", "rt_queue_synchronize",
 ]
 
 
@@ -136,6 +137,11 @@ def load_library(path: str = LIB_PATH):
         "rt_render_gather_all": [vp, vp, i32, vp, vp, i32, vp, vp, vp],
         "rt_comm_timing": [vp, vp, i32],
         "rt_comm_synchronize": [vp],
+        "rt_queue_create": [vp, i32, vp],
+        "rt_queue_destroy": [vp],
+        "rt_queue_submit": [vp, vp, vp, vp, vp, vp, vp, vp],
+        "rt_queue_wait": [vp, ctypes.c_uint64],
+        "rt_queue_synchronize": [vp],
         "rt_debug_assemble_rows": [vp, vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
                                    ctypes.c_uint32, ctypes.c_uint32, vp],
     }.items():
@@ -462,6 +468,40 @@ class Comm:
         t = GatherTiming()
         _check(_lib.rt_comm_timing(self._h, ctypes.byref(t), int(reset)))
         return t
+
+
+class Queue:
+    """Serving frame queue (rt_queue): frames of one context rendered into device framebuffers
+    with `depth` of them in flight on as many HIP streams."""
+
+    def __init__(self, ctx: Context, depth: int = 2):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        _check(load_library().rt_queue_create(ctx.handle, depth, ctypes.byref(self._h)))
+
+    def submit(self, dscene: "DeviceScene", opts: RenderOpts, d_hdr64: int | None = None,
+               d_hdr32: int | None = None, d_ldr: int | None = None) -> int:
+        t = ctypes.c_uint64()
+        _check(_lib.rt_queue_submit(self._h, dscene._h, dscene.camera.ctypes.data,
+                                    ctypes.byref(opts), d_hdr64, d_hdr32, d_ldr, ctypes.byref(t)))
+        return t.value
+
+    def wait(self, ticket: int):
+        _check(_lib.rt_queue_wait(self._h, ticket))
+
+    def synchronize(self):
+        _check(_lib.rt_queue_synchronize(self._h))
+
+    def close(self):
+        if self._h:
+            _lib.rt_queue_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def render_gather_all(comms: list, scenes: list, opts: RenderOpts, outputs: int,

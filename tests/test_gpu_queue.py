@@ -1,0 +1,91 @@
+"""The serving frame queue (rt_queue, include/rt_capi.h): frames with several in flight on
+separate HIP streams are the frames rt_render gives — the reference's, at full size — including
+the per-camera packet image created by one stream's frame and read by another's."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from raytracingengine_amd import capi
+from raytracingengine_amd.configs import make_config
+
+pytestmark = pytest.mark.gpu
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_queue_frames_equal_synchronous_renders(ctx, depth):
+    """Alternating camera positions, frames in flight on `depth` streams, each into its own
+    framebuffers: every frame equals the synchronous render of its camera (HDR bits, bytes)."""
+    sc = make_config("c3", 480, 270)
+    ds = ctx.scene(sc)
+    q = capi.Queue(ctx, depth)
+    W, H = sc.camera.width, sc.camera.height
+    base = ds.camera["position"][0].copy()
+    cams = [base, base + (0.5, -0.25, 1.0)]
+    try:
+        ref = []
+        for c in cams:
+            ds.camera["position"][0] = c
+            ref.append(ds.render(hdr64=True, tonemap=1))
+        n = 8
+        bufs = [(torch.empty(H * W * 3, dtype=torch.float64, device="cuda"),
+                 torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")) for _ in range(n)]
+        opts = capi.default_opts(tonemap=1)
+        tickets = []
+        for i in range(n):
+            ds.camera["position"][0] = cams[i % 2]
+            h, l = bufs[i]
+            tickets.append(q.submit(ds, opts, h.data_ptr(), None, l.data_ptr()))
+        assert tickets == list(range(n))
+        for i in range(n):
+            q.wait(tickets[i])
+            h, l = bufs[i]
+            r = ref[i % 2]
+            assert np.array_equal(h.cpu().numpy().reshape(H, W, 3), r["hdr64"]), i
+            assert np.array_equal(l.cpu().numpy().reshape(H, W, 3), r["ldr"]), i
+        q.synchronize()
+    finally:
+        ds.camera["position"][0] = base
+        q.close()
+        ds.close()
+
+
+def test_queue_full_c2_matches_reference(ctx, golden):
+    """The bench's frame (C2 1920x1080, f64 HDR + fused Reinhard) through a depth-2 queue, four
+    frames on two framebuffer sets: each the reference's frame (SHA-256 of HDR and bytes)."""
+    info = golden["meta"]["scenes"]["c2_full"]
+    sc = make_config("c2")
+    ds = ctx.scene(sc)
+    q = capi.Queue(ctx, 2)
+    W, H = sc.camera.width, sc.camera.height
+    bufs = [(torch.empty(H * W * 3, dtype=torch.float64, device="cuda"),
+             torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")) for _ in range(2)]
+    opts = capi.default_opts(tonemap=1)
+    try:
+        for rnd in range(2):
+            ts = [q.submit(ds, opts, h.data_ptr(), None, l.data_ptr()) for h, l in bufs]
+            for t, (h, l) in zip(ts, bufs):
+                q.wait(t)
+                assert _sha(h.cpu().numpy()) == info["image_sha256"], (rnd, t)
+                assert _sha(l.cpu().numpy()) == info["ldr_sha256"]["reinhard_simple"], (rnd, t)
+    finally:
+        q.close()
+        ds.close()
+
+
+def test_queue_rejects_bad_arguments(ctx):
+    with pytest.raises(capi.RtError) as e:
+        capi.Queue(ctx, 0)
+    assert e.value.status == capi.RT_ERR_INVALID_ARG
+    q = capi.Queue(ctx, 2)
+    try:
+        with pytest.raises(capi.RtError) as e:
+            q.wait(0)                       # nothing submitted yet
+        assert e.value.status == capi.RT_ERR_INVALID_ARG
+    finally:
+        q.close()
