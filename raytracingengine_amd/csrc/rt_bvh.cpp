@@ -187,3 +187,84 @@ void build_triangle_bvh(const double* tri, int nt, std::vector<double>& nodes,
 }
 
 }  // namespace rtamd
+
+namespace rtamd {
+
+// Spatial chunks of spheres for the packet kernel's culls (rt_packet.hip): a permutation that
+// puts spheres close together into the same 64-sphere chunk (recursive splits of the centre
+// bounds along their longest axis, left parts a multiple of 64), and a bounding sphere per chunk
+// that contains every sphere of the chunk.  A cull whose bound excludes a chunk's bounding
+// sphere excludes every sphere in it, so the chunk's lane-parallel pass is skipped.
+void build_sphere_chunks(const double* sph, int ns, std::vector<int32_t>& perm,
+                         std::vector<double>& bounds) {
+    perm.resize(static_cast<size_t>(ns));
+    for (int i = 0; i < ns; ++i) perm[static_cast<size_t>(i)] = i;
+    auto c = [&](int i, int k) { return sph[static_cast<size_t>(kSphStride) * i + k]; };
+    std::vector<std::pair<int, int>> todo{{0, ns}};
+    while (!todo.empty()) {
+        const auto [lo, hi] = todo.back();
+        todo.pop_back();
+        const int n = hi - lo;
+        if (n <= 64) continue;
+        Box b;
+        for (int j = lo; j < hi; ++j) {
+            const double p[3] = {c(perm[j], 0), c(perm[j], 1), c(perm[j], 2)};
+            if (std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2])) b.add(p);
+        }
+        int axis = 0;
+        for (int k = 1; k < 3; ++k)
+            if (b.hi[k] - b.lo[k] > b.hi[axis] - b.lo[axis]) axis = k;
+        const int chunks = (n + 63) / 64;
+        const int left = 64 * ((chunks + 1) / 2);
+        // non-finite centres sort last; ties by index (deterministic order)
+        auto key = [&](int i) { const double v = c(i, axis); return std::isfinite(v) ? v : INFINITY; };
+        std::nth_element(perm.begin() + lo, perm.begin() + lo + left, perm.begin() + hi,
+                         [&](int a, int b2) {
+                             const double ka = key(a), kb = key(b2);
+                             return ka < kb || (ka == kb && a < b2);
+                         });
+        todo.push_back({lo, lo + left});
+        todo.push_back({lo + left, hi});
+    }
+    const int nb = (ns + 63) / 64;
+    bounds.assign(static_cast<size_t>(nb) * 4, 0.0);
+    for (int ch = 0; ch < nb; ++ch) {
+        const int lo = 64 * ch, hi = std::min(ns, lo + 64);
+        Box b;
+        bool finite = true;
+        for (int j = lo; j < hi; ++j) {
+            const int i = perm[static_cast<size_t>(j)];
+            const double r = std::sqrt(c(i, 3));
+            const double p[3] = {c(i, 0), c(i, 1), c(i, 2)};
+            if (!(std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]) &&
+                  std::isfinite(r))) {
+                finite = false;
+                break;
+            }
+            const double l[3] = {p[0] - r, p[1] - r, p[2] - r}, h[3] = {p[0] + r, p[1] + r, p[2] + r};
+            b.add(l);
+            b.add(h);
+        }
+        double* o = &bounds[static_cast<size_t>(ch) * 4];
+        if (!finite) {  // a chunk with a non-finite sphere is never culled
+            o[0] = o[1] = o[2] = 0.0;
+            o[3] = INFINITY;
+            continue;
+        }
+        double cen[3], R = 0.0;
+        for (int k = 0; k < 3; ++k) cen[k] = 0.5 * (b.lo[k] + b.hi[k]);
+        for (int j = lo; j < hi; ++j) {
+            const int i = perm[static_cast<size_t>(j)];
+            const double dx = c(i, 0) - cen[0], dy = c(i, 1) - cen[1], dz = c(i, 2) - cen[2];
+            R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + std::sqrt(c(i, 3)));
+        }
+        // host rounding: far below 1e-9 of the magnitudes
+        const double mag = std::fabs(cen[0]) + std::fabs(cen[1]) + std::fabs(cen[2]) + R;
+        o[0] = cen[0];
+        o[1] = cen[1];
+        o[2] = cen[2];
+        o[3] = R * (1.0 + 1e-9) + 1e-9 * mag;
+    }
+}
+
+}  // namespace rtamd

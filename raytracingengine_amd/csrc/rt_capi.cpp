@@ -146,6 +146,10 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
         p.bvh_tri = reinterpret_cast<const int32_t*>(base + sc->off_bvh_tri);
     }
     p.lt = base + sc->off_lt;
+    if (sc->ns >= kSphChunkMin) {
+        p.sph_bnd = base + sc->off_sbnd;
+        p.sph_perm = reinterpret_cast<const int32_t*>(base + sc->off_sperm);
+    }
     p.ns = sc->ns;
     p.np = sc->np;
     p.nt = sc->nt;
@@ -525,6 +529,19 @@ rt_status rt_scene_create(rt_context* ctx, const rt_scene_desc* d, rt_scene** ou
         std::memcpy(&h[sc->off_bvh], nodes.data(), nodes.size() * sizeof(double));
         std::memcpy(&h[sc->off_bvh_tri], order.data(), order.size() * sizeof(int32_t));
         sc->bvh_nodes = static_cast<int32_t>(nodes.size() / kBvhNodeStride);
+    }
+
+    // spatial sphere chunks of the packet kernel's culls: permutation (packed two per double
+    // slot) and one bounding sphere per chunk
+    if (sc->ns >= kSphChunkMin) {
+        std::vector<int32_t> perm;
+        std::vector<double> bnd;
+        build_sphere_chunks(&h[sc->off_sph], sc->ns, perm, bnd);
+        sc->off_sbnd = (h.size() + 1) & ~size_t(1);
+        sc->off_sperm = sc->off_sbnd + bnd.size();
+        h.resize(sc->off_sperm + (perm.size() + 1) / 2 + 2, 0.0);
+        std::memcpy(&h[sc->off_sbnd], bnd.data(), bnd.size() * sizeof(double));
+        std::memcpy(&h[sc->off_sperm], perm.data(), perm.size() * sizeof(int32_t));
     }
 
     hipError_t e = sc->buf.ensure(h.size() * sizeof(double));

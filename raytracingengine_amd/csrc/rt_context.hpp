@@ -89,6 +89,7 @@ struct rt_scene {
     rt_area_light area{};
     size_t off_bvh = 0, off_bvh_tri = 0;  // triangle BVH, when bvh_nodes > 0
     int32_t bvh_nodes = 0;
+    size_t off_sperm = 0, off_sbnd = 0;   // sphere chunks, when ns >= kSphChunkMin
     // Packet-kernel LDS images, one per camera position this scene was rendered from more than
     // once (the image depends on the spheres, planes, point lights and camera position only).  An
     // entry is written once, by packet_image_kernel on the stream of the render that created

@@ -70,7 +70,16 @@ struct TraceParams {
     const double* bvh;       // triangle BVH nodes (rt_bvh.cpp), or null: test every triangle
     const int32_t* bvh_tri;  // triangle ids in leaf order
     const double* pk_image;  // packet kernel: LDS image of this scene + camera, or null
+    // packet kernel, ns >= kSphChunkMin: spatial sphere order and chunk bounds (build_sphere_chunks)
+    const int32_t* sph_perm;
+    const double* sph_bnd;
 };
+
+// Host: the spatial sphere chunks of the packet kernel's culls (rt_bvh.cpp): perm[sorted] =
+// original index, bounds = one bounding sphere (cx cy cz R) per 64 sorted spheres.
+constexpr int kSphChunkMin = 65;  // scenes with fewer spheres have a single chunk (no order)
+void build_sphere_chunks(const double* sph, int ns, std::vector<int32_t>& perm,
+                         std::vector<double>& bounds);
 
 // Host: builds the triangle BVH over the uploaded triangle records (kTriStride doubles each).
 void build_triangle_bvh(const double* tri, int nt, std::vector<double>& nodes,

@@ -123,7 +123,11 @@ struct PacketScene {
     const double* mat;   // HBM: material table [spheres | planes | triangles]
     const double* bvh;   // HBM: triangle BVH, or null
     const int32_t* bvh_tri;
-    int ns, np, nt, nl;
+    // scenes with >= kSphChunkMin spheres: spheres are in spatial-chunk order (sph, rad, cone,
+    // pre), chunk c's bounding sphere is pseudo-sphere ns + c of sph / rad / cone (nb of them),
+    // and orig[i] is sorted sphere i's index in the scene (material table, closest-hit ties)
+    const int32_t* orig;
+    int ns, np, nt, nl, nb;
 };
 
 // Closest hit of the packet kernel: t and the primitive's index in the material table order
@@ -205,19 +209,23 @@ __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 axis, 
     const float sn = sqrt_f32(fmaxf(0.0f, 1.0f - cs * cs)) * (1.0f + 1e-5f);  // rounded up
     const float ax = static_cast<float>(axis.x), ay = static_cast<float>(axis.y),
                 az = static_cast<float>(axis.z);
+    auto test = [&](int k) {
+        const float4 a = reinterpret_cast<const float4*>(S.cone)[2 * k];
+        const float4 b = reinterpret_cast<const float4*>(S.cone)[2 * k + 1];
+        const float q = a.w, rr = b.x, dv = b.y, slack = b.z;
+        // θ + β ≥ π, or the axis is outside the cone around C−o (NaN q: always kept)
+        return !(q > -cs * dv + slack) ||
+               !(dot3f(a.x, a.y, a.z, ax, ay, az) < cs * q - sn * rr - slack);
+    };
+    uint64_t live = ~0ull;  // chunks whose bounding sphere the cone may meet
+    if constexpr (MAXC > 1)
+        if (S.nb > 0) live = __ballot(lane < S.nb && test(S.ns + lane));
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
+        M.m[c] = 0ull;
+        if (!((live >> c) & 1ull)) continue;  // uniform: no sphere of the chunk is in the cone
         const int k = c * 64 + lane;
-        bool keep = false;
-        if (k < S.ns) {
-            const float4 a = reinterpret_cast<const float4*>(S.cone)[2 * k];
-            const float4 b = reinterpret_cast<const float4*>(S.cone)[2 * k + 1];
-            const float q = a.w, rr = b.x, dv = b.y, slack = b.z;
-            // θ + β ≥ π, or the axis is outside the cone around C−o (NaN q: always kept)
-            keep = !(q > -cs * dv + slack) ||
-                   !(dot3f(a.x, a.y, a.z, ax, ay, az) < cs * q - sn * rr - slack);
-        }
-        M.m[c] = __ballot(keep);
+        M.m[c] = __ballot(k < S.ns && test(k));
     }
     M.pm = ~0ull;
     return M;
@@ -243,32 +251,35 @@ __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, 
     const float sl2 = dot3f(sx, sy, sz, sx, sy, sz);
     const float inv_sl2 = 1.0f / sl2;  // wave-uniform; only read when sl2 > 0
     const float Rc = fmaxf(R, f32_up(RL)) + f32_up(fabs(bias)) * 1.001f;  // |n| ≤ 1 + 2ε
+    auto test = [&](int k) {
+        const double* s = S.sph + kSphStride * k;
+        const float r = f32_up(S.rad[k]);
+        const float vx = static_cast<float>(s[0] - c.x), vy = static_cast<float>(s[1] - c.y),
+                    vz = static_cast<float>(s[2] - c.z);
+        const float vs = dot3f(vx, vy, vz, sx, sy, sz);
+        const float vv = dot3f(vx, vy, vz, vx, vy, vz);
+        float d2;
+        if (!(vs > 0.0f) || !(sl2 > 0.0f)) {
+            d2 = vv;
+        } else if (!(vs < sl2)) {
+            const float wx = vx - sx, wy = vy - sy, wz = vz - sz;
+            d2 = dot3f(wx, wy, wz, wx, wy, wz);
+        } else {
+            d2 = vv - (vs * vs) * inv_sl2;  // one more rounding than a division: ≪ slack
+        }
+        const float lim = (r + Rc) * (1.0f + static_cast<float>(kCullRel));
+        const float far = static_cast<float>(kFarRatio) * r - Rc;
+        return !(d2 > lim * lim + kF32Slack * (vv + sl2)) || !(far > 0.0f) || !(vv <= far * far);
+    };
+    uint64_t live = ~0ull;  // chunks whose bounding sphere the capsule may meet
+    if constexpr (MAXC > 1)
+        if (S.nb > 0) live = __ballot(lane < S.nb && test(S.ns + lane));
 #pragma unroll
     for (int ch = 0; ch < MAXC; ++ch) {
+        M.m[ch] = 0ull;
+        if (!((live >> ch) & 1ull)) continue;  // uniform: the capsule misses the whole chunk
         const int k = ch * 64 + lane;
-        bool keep = false;
-        if (k < S.ns) {
-            const double* s = S.sph + kSphStride * k;
-            const float r = f32_up(S.rad[k]);
-            const float vx = static_cast<float>(s[0] - c.x), vy = static_cast<float>(s[1] - c.y),
-                        vz = static_cast<float>(s[2] - c.z);
-            const float vs = dot3f(vx, vy, vz, sx, sy, sz);
-            const float vv = dot3f(vx, vy, vz, vx, vy, vz);
-            float d2;
-            if (!(vs > 0.0f) || !(sl2 > 0.0f)) {
-                d2 = vv;
-            } else if (!(vs < sl2)) {
-                const float wx = vx - sx, wy = vy - sy, wz = vz - sz;
-                d2 = dot3f(wx, wy, wz, wx, wy, wz);
-            } else {
-                d2 = vv - (vs * vs) * inv_sl2;  // one more rounding than a division: ≪ slack
-            }
-            const float lim = (r + Rc) * (1.0f + static_cast<float>(kCullRel));
-            const float far = static_cast<float>(kFarRatio) * r - Rc;
-            keep = !(d2 > lim * lim + kF32Slack * (vv + sl2)) || !(far > 0.0f) ||
-                   !(vv <= far * far);
-        }
-        M.m[ch] = __ballot(keep);
+        M.m[ch] = __ballot(k < S.ns && test(k));
     }
     // Planes (feature kFeatPlanes, scenes with three or more, where one lane-parallel test costs
     // less than the per-lane plane tests it saves): a plane with the capsule strictly on one
@@ -301,25 +312,38 @@ __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, 
     return M;
 }
 
+// The running closest hit takes candidate i at t when the reference's in-order loop with strict
+// '<' (Shape.h:36) would end on it: t < best, or — when the spheres are in spatial-chunk order
+// (ORD, orig[] = scene indices) — t == best with a lower scene index.
+template <bool ORD>
+__device__ __forceinline__ void take_closest(double t, int i, const int32_t* orig, bool& found,
+                                             double& best, int& prim) {
+    bool take = !found || t < best;
+    if constexpr (ORD) take = take || (t == best && orig[i] < orig[prim]);
+    if (take) {
+        found = true;
+        best = t;
+        prim = i;
+    }
+}
+
 // Root selection of Sphere::Intersect (Shape.h:84-97) folded into the running closest.
 // Requires two_a > 0 (then t0 ≤ t1 exactly); divisions are skipped when the candidate
 // provably cannot be strictly closer than `best`.
+template <bool ORD>
 __device__ __forceinline__ void sphere_roots(double b, double disc, double two_a, int i,
-                                             bool& found, double& best, int& prim) {
+                                             const int32_t* orig, bool& found, double& best,
+                                             int& prim) {
     if (disc < 0.0) return;
     const double sq = sqrt(disc);
     const double n0 = -b - sq;
-    if (found && n0 > (best * two_a) * kNoWin) return;  // t1 >= t0 >= best
+    if (found && n0 > (best * two_a) * kNoWin) return;  // t1 >= t0 > best (strictly)
     double t = n0 / two_a;
     if (t < 1e-6) {
         t = (-b + sq) / two_a;
         if (t < 1e-6) return;
     }
-    if (!found || t < best) {
-        found = true;
-        best = t;
-        prim = i;
-    }
+    take_closest<ORD>(t, i, orig, found, best, prim);
 }
 
 // sphere_roots through the sqrt/division cores (rt_device.hpp), r2a = rcp_refined(two_a) with
@@ -327,8 +351,10 @@ __device__ __forceinline__ void sphere_roots(double b, double disc, double two_a
 // a numerator |n| ≥ 2^-900 divides exactly, and a smaller one gives |t| < 2^-790 both exactly
 // and through the core, so the 1e-6 test (the only use of such a root) decides alike.  Other
 // discriminants take the literal path.  t0 ≤ t1 as in sphere_roots.
+template <bool ORD>
 __device__ __forceinline__ void sphere_roots_core(double b, double disc, double two_a, double r2a,
-                                                  int i, bool& found, double& best, int& prim) {
+                                                  int i, const int32_t* orig, bool& found,
+                                                  double& best, int& prim) {
     if (disc < 0.0) return;
     double t;
     if (disc >= 0x1p-767 && disc <= 0x1.fffffffffffffp+1023) {
@@ -346,16 +372,14 @@ __device__ __forceinline__ void sphere_roots_core(double b, double disc, double 
             if (t < 1e-6) return;
         }
     }
-    if (!found || t < best) {
-        found = true;
-        best = t;
-        prim = i;
-    }
+    take_closest<ORD>(t, i, orig, found, best, prim);
 }
 
 // The reference's literal root selection, for degenerate directions (2a not > 0).
+template <bool ORD>
 __device__ __forceinline__ void sphere_roots_literal(double b, double disc, double two_a, int i,
-                                                     bool& found, double& best, int& prim) {
+                                                     const int32_t* orig, bool& found,
+                                                     double& best, int& prim) {
     if (disc < 0.0) return;
     const double sq = sqrt(disc);
     double t0 = (-b - sq) / two_a;
@@ -370,11 +394,7 @@ __device__ __forceinline__ void sphere_roots_literal(double b, double disc, doub
         t = t1;
         if (t < 1e-6) return;
     }
-    if (!found || t < best) {
-        found = true;
-        best = t;
-        prim = i;
-    }
+    take_closest<ORD>(t, i, orig, found, best, prim);
 }
 
 // Plane::Intersect (Shape.h:149-159) given num = (p − o)·n and denom = n·d.
@@ -454,7 +474,7 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
                 const double* q = S.pre + 4 * i;
                 const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
                 const double disc = b * b - four_a * q[3];
-                sphere_roots_core(b, disc, two_a, r2a, i, found, best, prim);
+                sphere_roots_core<(MAXC > 1)>(b, disc, two_a, r2a, i, S.orig, found, best, prim);
             }
         }
     } else {
@@ -468,8 +488,8 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
                 const double* q = S.pre + 4 * i;
                 const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
                 const double disc = b * b - four_a * q[3];
-                if (regular) sphere_roots(b, disc, two_a, i, found, best, prim);
-                else sphere_roots_literal(b, disc, two_a, i, found, best, prim);
+                if (regular) sphere_roots<(MAXC > 1)>(b, disc, two_a, i, S.orig, found, best, prim);
+                else sphere_roots_literal<(MAXC > 1)>(b, disc, two_a, i, S.orig, found, best, prim);
             }
         }
     }
@@ -507,8 +527,8 @@ __device__ __forceinline__ bool closest_masked(const PacketScene& S, const Masks
             const double b = 2.0 * dot(oc, d);
             const double cc = dot(oc, oc) - s[3];
             const double disc = b * b - four_a * cc;
-            if (regular) sphere_roots(b, disc, two_a, i, found, best, prim);
-            else sphere_roots_literal(b, disc, two_a, i, found, best, prim);
+            if (regular) sphere_roots<(MAXC > 1)>(b, disc, two_a, i, S.orig, found, best, prim);
+            else sphere_roots_literal<(MAXC > 1)>(b, disc, two_a, i, S.orig, found, best, prim);
         }
     }
     for (int i = 0; i < S.np; ++i) {
@@ -522,8 +542,13 @@ __device__ __forceinline__ bool closest_masked(const PacketScene& S, const Masks
     return found;
 }
 
+template <int MAXC>
 __device__ __forceinline__ const double* pk_material(const PacketScene& S, const PkHit& h) {
-    return S.mat + kMatStride * h.prim;  // the table is [spheres | planes | triangles]
+    // the table is [spheres | planes | triangles] in scene order; spheres in chunk order (MAXC
+    // > 1: > 64 spheres) map back to it
+    int m = h.prim;
+    if constexpr (MAXC > 1) m = h.prim < S.ns ? S.orig[h.prim] : h.prim;
+    return S.mat + kMatStride * m;
 }
 
 __device__ __forceinline__ d3 pk_normal(const PacketScene& S, const PkHit& h, d3 p) {
@@ -561,7 +586,7 @@ __device__ __forceinline__ double pk_transmittance(const PacketScene& S, const M
             continue;
         }
         if (traveled + t >= max_dist) break;
-        T *= sclamp(pk_material(S, h)[5], 0.0, 1.0);
+        T *= sclamp(pk_material<MAXC>(S, h)[5], 0.0, 1.0);
         o = (o + d * t) + d * bias;
         traveled += t + bias;
     }
@@ -791,7 +816,7 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     if (T <= bias) return;
     diff = diff + ((E * inv_d2) * ndl) * T;
     if constexpr ((FEAT & kFeatSpec) != 0) {
-        const double* m = pk_material(S, h);
+        const double* m = pk_material<MAXC>(S, h);
         if (m[5] <= 0.0 && m[4] > 0.0) {
             const d3 H = unit(L + view);
             const double ndh = smax(0.0, dot(n, H));
@@ -807,27 +832,49 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
 // aligned arrays): spheres, camera-cone terms, culling radii, camera-ray sphere constants,
 // planes with their camera numerators, point lights, camera-ray plane normals.  Formed by each
 // workgroup into LDS, or once per (scene, camera) into HBM by packet_image_kernel and copied.
+// With >= kSphChunkMin spheres the spheres are in spatial-chunk order, each chunk's bounding
+// sphere follows them as a pseudo-sphere in the sphere / cone / radius arrays, and the scene
+// index of every sorted sphere closes the image.
+__host__ __device__ inline int pk_chunk_bounds(int ns) { return ns >= kSphChunkMin ? (ns + 63) / 64 : 0; }
 __host__ __device__ inline size_t pk_image_bytes(int ns, int np, int nl) {
-    const size_t b = sizeof(double) * (static_cast<size_t>(kSphStride + 1 + 4 + 4) * ns +
+    const size_t nsb = static_cast<size_t>(ns) + pk_chunk_bounds(ns);
+    const size_t b = sizeof(double) * (static_cast<size_t>(kSphStride + 1 + 4) * nsb +
+                                       static_cast<size_t>(4) * ns +
                                        static_cast<size_t>(kPlStride + 4) * np +
-                                       static_cast<size_t>(kLtStride) * nl);
+                                       static_cast<size_t>(kLtStride) * nl) +
+                     (pk_chunk_bounds(ns) ? sizeof(int32_t) * ns : 0);
     return (b + 15) / 16 * 16;
 }
 
 __device__ __forceinline__ void pk_build_image(const TraceParams& P, double* img, int tid,
                                                int nthreads) {
-    const int ns = P.ns, np = P.np, nl = P.nl;
-    double* s_sph = img;                                          // 32·ns bytes
-    float* s_cone = reinterpret_cast<float*>(s_sph + kSphStride * ns);  // 16-byte aligned
-    double* s_rad = s_sph + (kSphStride + 4) * ns;
-    double* s_pre = s_rad + ns;
+    const int ns = P.ns, np = P.np, nl = P.nl, nb = pk_chunk_bounds(ns), nsb = ns + nb;
+    double* s_sph = img;                                          // 32·nsb bytes
+    float* s_cone = reinterpret_cast<float*>(s_sph + kSphStride * nsb);  // 16-byte aligned
+    double* s_rad = s_sph + (kSphStride + 4) * nsb;
+    double* s_pre = s_rad + nsb;
     double* s_pl = s_pre + 4 * ns;
     double* s_lt = s_pl + kPlStride * np;
     double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
+    int32_t* s_orig = reinterpret_cast<int32_t*>(s_pln + 4 * np);  // nb > 0 only
     const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    for (int i = tid; i < kSphStride * ns; i += nthreads) s_sph[i] = P.sph[i];
+    const int32_t* perm = nb ? P.sph_perm : nullptr;
+    for (int i = tid; i < kSphStride * ns; i += nthreads)
+        s_sph[i] = P.sph[kSphStride * (perm ? perm[i / kSphStride] : i / kSphStride) + i % kSphStride];
+    for (int i = tid; i < nb; i += nthreads) {  // chunk bounds as pseudo-spheres ns + c
+        const double* q = P.sph_bnd + 4 * i;
+        double* o = s_sph + kSphStride * (ns + i);
+        o[0] = q[0];
+        o[1] = q[1];
+        o[2] = q[2];
+        o[3] = q[3] * q[3];
+        s_rad[ns + i] = q[3];
+        cone_terms(o, q[3], cam, s_cone + 8 * (ns + i));
+    }
     for (int i = tid; i < ns; i += nthreads) {
-        const double* s = P.sph + kSphStride * i;
+        const int si = perm ? perm[i] : i;
+        if (perm) s_orig[i] = si;
+        const double* s = P.sph + kSphStride * si;
         s_rad[i] = sqrt(s[3]);  // culling radius (only ever used with a margin)
         cone_terms(s, s_rad[i], cam, s_cone + 8 * i);
         // camera-ray constants of Sphere::Intersect (Shape.h:73,77)
@@ -868,14 +915,15 @@ template <int MAXC, int FEAT, bool COUNT, bool MULTI, int WGY>  // MULTI = false
 __global__ __launch_bounds__(64 * kWgWavesX * WGY, ((FEAT == 0 || FEAT == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
-    const int ns = P.ns, np = P.np, nl = P.nl;
-    double* s_sph = smem;                                         // 32·ns bytes
-    float* s_cone = reinterpret_cast<float*>(s_sph + kSphStride * ns);  // 16-byte aligned
-    double* s_rad = s_sph + (kSphStride + 4) * ns;
-    double* s_pre = s_rad + ns;
+    const int ns = P.ns, np = P.np, nl = P.nl, nb = pk_chunk_bounds(ns), nsb = ns + nb;
+    double* s_sph = smem;                                         // 32·nsb bytes
+    float* s_cone = reinterpret_cast<float*>(s_sph + kSphStride * nsb);  // 16-byte aligned
+    double* s_rad = s_sph + (kSphStride + 4) * nsb;
+    double* s_pre = s_rad + nsb;
     double* s_pl = s_pre + 4 * ns;
     double* s_lt = s_pl + kPlStride * np;
     double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
+    const int32_t* s_orig = reinterpret_cast<const int32_t*>(s_pln + 4 * np);
     const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     if (P.pk_image) {  // the image of this scene and camera, formed once (packet_image_kernel)
         const float4* src = reinterpret_cast<const float4*>(P.pk_image);
@@ -902,6 +950,8 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, ((FEAT == 0 || FEAT == kFeatA
     S.np = np;
     S.nt = P.nt;
     S.nl = nl;
+    S.nb = nb;
+    S.orig = nb ? s_orig : nullptr;
     const int nchunks = (ns + 63) / 64;
 
     const int lane = tid & 63, wave = tid >> 6;
@@ -1058,7 +1108,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, ((FEAT == 0 || FEAT == kFeatA
                 }
             }
             if (hit) {
-                const double* m = pk_material(S, h);
+                const double* m = pk_material<MAXC>(S, h);
                 const d3 local = hmul(mk(m[0], m[1], m[2]), diff) + spec * m[4];
                 const double tr = sclamp(m[5], 0.0, 1.0);
                 d3 fin = mk(0.0, 0.0, 0.0);

@@ -502,6 +502,33 @@ def test_edge_plane_cull_variants(ctx, oracle, kind):
     assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)
 
 
+@pytest.mark.parametrize("n_spheres,aa", [(100, 1), (300, 1), (130, 2)])
+def test_sphere_chunks_keep_scene_order_ties(ctx, oracle, n_spheres, aa):
+    """Scenes with > 64 spheres run the packet kernel on spheres in spatial-chunk order
+    (rt_bvh.cpp build_sphere_chunks): coincident duplicate spheres with different materials —
+    some in one chunk, some split across chunks — must still resolve to the lower scene index,
+    as the reference's in-order loop with strict '<' does (Scene.h:218-257, Shape.h:36)."""
+    from raytracingengine_amd.configs import SplitMix64
+    rng = SplitMix64(0xC0FFEE + n_spheres)
+    sc = _scene(160, 90, aa=aa)
+    sc.add_plane((0, -9, 0), (0, 1, 0), Material((0.8, 0.8, 0.8)))
+    placed = []
+    for i in range(n_spheres):
+        if i % 9 == 8 and placed:           # a duplicate of an earlier sphere, new colour
+            c, r = placed[int(rng.uniform(0, len(placed)))]
+        else:
+            c = (rng.uniform(-12, 12), rng.uniform(-7, 7), rng.uniform(0, 16))
+            r = rng.uniform(0.4, 1.6)
+            placed.append((c, r))
+        sc.add_sphere(c, r, Material((rng.uniform(0.1, 1), rng.uniform(0.1, 1), rng.uniform(0.1, 1))))
+    sc.add_light((3, 11, -6), (1, 1, 1), 200)
+    sc.add_light((-7, 8, -12), (1, 0.9, 0.8), 120)
+    out = _render(ctx, sc, hdr64=True, stats=True, seed=11)
+    ref, nt, ns = oracle.render(sc, seed=11)
+    assert np.array_equal(out["hdr64"], ref)
+    assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)
+
+
 def test_invalid_arguments_raise(ctx):
     sc = make_config("c2", 32, 16)
     ds = ctx.scene(sc)
