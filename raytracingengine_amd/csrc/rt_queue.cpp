@@ -18,8 +18,7 @@ struct rt_queue {
     rt_context* ctx = nullptr;
     std::vector<hipStream_t> streams;
     std::vector<hipEvent_t> done;   // per slot: recorded after the slot's latest frame
-    std::vector<uint64_t> ticket;   // per slot: the ticket of that frame
-    uint64_t next = 0;              // ticket of the next submitted frame
+    uint64_t next = 0;              // ticket of the next submitted frame (slot = ticket % depth)
 };
 
 extern "C" {
@@ -43,7 +42,6 @@ rt_status rt_queue_create(rt_context* ctx, int depth, rt_queue** out) {
             rt_queue_destroy(q);
             return hip_fail(err, "rt_queue_create");
         }
-        q->ticket.push_back(0);
     }
     *out = q;
     return RT_OK;
@@ -77,7 +75,6 @@ rt_status rt_queue_submit(rt_queue* q, const rt_scene* sc, const rt_camera* cam,
     ctx->stream = saved;
     if (st != RT_OK) return st;
     if (e != hipSuccess) return hip_fail(e, "rt_queue_submit");
-    q->ticket[slot] = q->next;
     if (ticket_out) *ticket_out = q->next;
     q->next += 1;
     return RT_OK;
