@@ -317,7 +317,8 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
             RT_HIP(ctx->wf_ctl.ensure(sizeof(WfCtl)));
             const WfArena A = wf_arena_layout(ctx->wf.ptr, n0, cap,
                                               static_cast<WfCtl*>(ctx->wf_ctl.ptr));
-            RT_HIP(launch_wavefront(p, path, A, lds, lds_bytes, ctx->stream));
+            RT_HIP(lean_generic ? lean::launch_wavefront(p, path, A, lds, lds_bytes, ctx->stream)
+                                : launch_wavefront(p, path, A, lds, lds_bytes, ctx->stream));
             wavefront = true;
         }
     }

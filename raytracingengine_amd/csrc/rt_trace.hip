@@ -30,18 +30,22 @@ template <int PATH, bool COUNT, bool LDS, int MINW = 2, bool SINGLE = false>
 __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParams P) {
     extern __shared__ double smem[];
     const int tid = threadIdx.y * kTileW + threadIdx.x;
-    const SceneView S = stage_scene<LDS>(P, smem, tid, kTileW * kTileH);
     const uint32_t x = blockIdx.x * kTileW + threadIdx.x;
     const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
     Counts cnt{0u, 0u};
     bool run = x < P.width && yl < P.rows;
-    if (run && P.redo) {
-        // fix-up pass of the wavefront renderer: only pixels with an incomplete sample tree
-        const size_t r0 = (static_cast<size_t>(yl) * P.width + x) * static_cast<size_t>(P.aa);
-        bool any = false;
-        for (int s = 0; s < P.aa; ++s) any = any || P.redo[r0 + s] != 0;
-        run = any;
+    if (P.redo) {  // uniform
+        // fix-up pass of the wavefront renderer: only pixels with an incomplete sample tree,
+        // and workgroups without one leave before staging the scene
+        if (run) {
+            const size_t r0 = (static_cast<size_t>(yl) * P.width + x) * static_cast<size_t>(P.aa);
+            bool any = false;
+            for (int s = 0; s < P.aa; ++s) any = any || P.redo[r0 + s] != 0;
+            run = any;
+        }
+        if (!__syncthreads_or(run)) return;
     }
+    const SceneView S = stage_scene<LDS>(P, smem, tid, kTileW * kTileH);
     if (run) {
         const uint32_t y = image_row(P, yl);
         const uint64_t pix = static_cast<uint64_t>(y) * P.width + x;

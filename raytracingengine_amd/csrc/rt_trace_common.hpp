@@ -518,7 +518,9 @@ __device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, 
         const double eta_t = m.ior;
         const double r0 = (eta_t - 1.0) / (eta_t + 1.0);
         const double f0 = r0 * r0;  // pow(x, 2.0)
-        double F = f0 + (1.0 - f0) * pow(1.0 - cos_t, 5.0);
+        // pow(1 - cosθ, 5) through pow_bp (rt_device.hpp: ≤ 2e-16 absolute on [0, 1], the
+        // libm pow out of line outside (0, 1.5)) instead of the inlined libm pow
+        double F = f0 + (1.0 - f0) * pow_bp(1.0 - cos_t, 5.0);
         const double eta = front ? (1.0 / eta_t) : (eta_t / 1.0);
         d3 rd = refract(inc, n, eta);
         if (length(rd) > bias) {

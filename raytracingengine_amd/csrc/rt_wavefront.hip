@@ -26,6 +26,11 @@
 #pragma clang fp contract(off)
 
 namespace rtamd {
+#ifdef RT_LEAN_GENERIC
+// rt_wavefront_lean.hip: the same level / fold / final kernels without the triangle / BVH and
+// area-light code (rt_trace_common.hpp), for scenes that have neither (rtamd::lean).
+namespace lean {
+#endif
 
 namespace {
 
@@ -49,9 +54,15 @@ __device__ __forceinline__ void level_range(const WfArena& A, int level, uint32_
     n = base >= A.cap ? 0u : min(want, A.cap - base);
 }
 
+// level kernels: 2 waves/SIMD, 3 in the lean build (213 → 168 VGPRs: glass 1.58 → 1.54 ms)
+#ifdef RT_LEAN_GENERIC
+constexpr int kWfLevelWaves = 3;
+#else
+constexpr int kWfLevelWaves = 2;
+#endif
 template <bool TREE, bool LDS>
-__global__ __launch_bounds__(kWfThreads, 2) void wf_level_kernel(TraceParams P, WfArena A,
-                                                              int level) {
+__global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(TraceParams P,
+                                                                             WfArena A, int level) {
     extern __shared__ double smem[];
     const SceneView S = stage_scene<LDS>(P, smem, threadIdx.x, kWfThreads);
     uint32_t base, n;
@@ -219,6 +230,7 @@ hipError_t launch_levels(const TraceParams& p, const WfArena& A, size_t lds_byte
 
 }  // namespace
 
+#ifndef RT_LEAN_GENERIC
 size_t wf_arena_bytes(size_t n0, size_t cap) {
     const size_t cap_r = cap - n0;
     return sizeof(double) * (5 * cap + 6 * cap_r) + sizeof(int32_t) * 2 * cap +
@@ -247,6 +259,7 @@ WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl) {
     A.ctl = ctl;
     return A;
 }
+#endif
 
 hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bool lds,
                             size_t lds_bytes, hipStream_t stream) {
@@ -260,10 +273,18 @@ hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bo
         e = lds ? launch_levels<false, true>(p, A, lds_bytes, stream)
                 : launch_levels<false, false>(p, A, lds_bytes, stream);
     if (e != hipSuccess) return e;
-    // fix-up: the per-pixel kernel for pixels whose sample trees overflowed the arena
+    // fix-up: the per-pixel kernel for pixels whose sample trees overflowed the arena (the lean
+    // build's own, rtamd::lean::launch_trace)
     TraceParams q = p;
     q.redo = A.redo;
-    return launch_trace(q, path, false, lds, lds_bytes, stream);
+#ifdef RT_LEAN_GENERIC
+    return rtamd::lean::launch_trace(q, path, false, lds, lds_bytes, stream);
+#else
+    return rtamd::launch_trace(q, path, false, lds, lds_bytes, stream);
+#endif
 }
 
+#ifdef RT_LEAN_GENERIC
+}  // namespace lean
+#endif
 }  // namespace rtamd

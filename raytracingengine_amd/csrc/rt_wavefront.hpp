@@ -33,5 +33,9 @@ size_t wf_arena_bytes(size_t n0, size_t cap);
 WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl);
 hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bool lds,
                             size_t lds_bytes, hipStream_t stream);
+namespace lean {  // rt_wavefront_lean.hip: scenes without triangles / area light
+hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bool lds,
+                            size_t lds_bytes, hipStream_t stream);
+}
 
 }  // namespace rtamd
