@@ -70,6 +70,10 @@ constexpr int kFeatAll = 31;
 #ifndef RT_PACKET_LEAN_WAVES
 #define RT_PACKET_LEAN_WAVES 4
 #endif
+// ... the triangle-only variants (BVH traversal; models without specular materials)
+#ifndef RT_PACKET_TRIS_WAVES
+#define RT_PACKET_TRIS_WAVES 4
+#endif
 // ... and the single-sample variants without Blinn-Phong / triangles (5 = at most 96 VGPRs)
 #ifndef RT_PACKET_AA1_WAVES
 #define RT_PACKET_AA1_WAVES 5
@@ -912,7 +916,7 @@ __device__ __forceinline__ void pk_build_image(const TraceParams& P, double* img
 }
 
 template <int MAXC, int FEAT, bool COUNT, bool MULTI, int WGY>  // MULTI = false: one sample (AA = 1)
-__global__ __launch_bounds__(64 * kWgWavesX * WGY, ((FEAT == 0 || FEAT == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1) void packet_direct_kernel(TraceParams P) {
+__global__ __launch_bounds__(64 * kWgWavesX * WGY, FEAT == kFeatTris ? RT_PACKET_TRIS_WAVES : (((FEAT == 0 || FEAT == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1)) void packet_direct_kernel(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
     const int ns = P.ns, np = P.np, nl = P.nl, nb = pk_chunk_bounds(ns), nsb = ns + nb;
@@ -1211,10 +1215,12 @@ hipError_t launch_packet_area(const TraceParams& p, bool count, size_t lds, int 
 template <int MAXC>
 static void launch_packet_maxc(const TraceParams& p, bool count, size_t lds, int feat,
                                hipStream_t stream) {
-    // three compiled feature sets: lean (the BASELINE C2-C4 shape), lean + area light (C5),
-    // and everything
+    // compiled feature sets: lean (the BASELINE C2-C4 shape), lean + plane culls (C3), lean +
+    // area light (C5, rt_packet_area.hip), triangles / models only (no Blinn-Phong, area light
+    // or Reinhard-Jodie), and everything
     if (feat == 0) launch_packet_variant<MAXC, 0>(p, count, lds, stream);
     else if (feat == kFeatPlanes) launch_packet_variant<MAXC, kFeatPlanes>(p, count, lds, stream);
+    else if (feat == kFeatTris) launch_packet_variant<MAXC, kFeatTris>(p, count, lds, stream);
     else launch_packet_variant<MAXC, kFeatAll>(p, count, lds, stream);
 }
 
