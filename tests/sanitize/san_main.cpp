@@ -1,6 +1,7 @@
 // tests/sanitize/san_main.cpp — host-code driver for the AddressSanitizer / UBSan build
 // (tests/test_sanitizers.py).  Exercises the host code on the path that runs outside the GPU:
 //   bvh <tri.bin> <n>          rtamd::build_triangle_bvh (csrc/rt_bvh.cpp) + structure checks
+//   chunks <sph.bin> <n>       rtamd::build_sphere_chunks (csrc/rt_bvh.cpp) + containment checks
 //   obj <file.obj>             rtamd::LoadObject (api/rtamd/obj.cpp)
 //   scene <file.txt>           rtamd::load_scene_file (api/rtamd/scenefile.hpp)
 //   oracle <dir> <rows>        oracle_render / tonemap / KAT entry points (oracle/rt_oracle.c)
@@ -159,6 +160,40 @@ int run_oracle(const std::string& dir, uint32_t rows) {
     return w == img.size() ? 0 : fail("write out.f64");
 }
 
+// The spatial sphere chunks of the packet kernel: a permutation, every sphere once, and each
+// 64-sphere chunk's bounding sphere containing every member sphere (or infinite).
+int run_chunks(const std::string& path, int ns) {
+    std::vector<char> raw = slurp(path);
+    if (raw.size() != size_t(ns) * rtamd::kSphStride * sizeof(double)) return fail("sph size");
+    std::vector<double> sph(raw.size() / sizeof(double));
+    std::memcpy(sph.data(), raw.data(), raw.size());
+    std::vector<int32_t> perm;
+    std::vector<double> bnd;
+    rtamd::build_sphere_chunks(sph.data(), ns, perm, bnd);
+    if (perm.size() != size_t(ns)) return fail("perm size");
+    const size_t nb = (size_t(ns) + 63) / 64;
+    if (bnd.size() != nb * 4) return fail("bounds size");
+    std::vector<int> seen(static_cast<size_t>(ns), 0);
+    for (int32_t i : perm) {
+        if (i < 0 || i >= ns) return fail("perm index");
+        seen[static_cast<size_t>(i)]++;
+    }
+    for (int s : seen)
+        if (s != 1) return fail("sphere not exactly once");
+    for (size_t c = 0; c < nb; ++c) {
+        const double* b = &bnd[c * 4];
+        for (size_t j = c * 64; j < std::min(size_t(ns), c * 64 + 64); ++j) {
+            const double* s = &sph[size_t(perm[j]) * rtamd::kSphStride];
+            const double r = std::sqrt(s[3]);
+            if (std::isinf(b[3]) && b[3] > 0) continue;
+            const double dx = s[0] - b[0], dy = s[1] - b[1], dz = s[2] - b[2];
+            if (!(std::sqrt(dx * dx + dy * dy + dz * dz) + r <= b[3])) return fail("sphere outside its chunk bound");
+        }
+    }
+    std::printf("chunks %d spheres %zu chunks\n", ns, nb);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -168,6 +203,7 @@ int main(int argc, char** argv) {
     }
     const std::string mode = argv[1];
     if (mode == "bvh" && argc == 4) return run_bvh(argv[2], std::atoi(argv[3]));
+    if (mode == "chunks" && argc == 4) return run_chunks(argv[2], std::atoi(argv[3]));
     if (mode == "obj") return run_obj(argv[2]);
     if (mode == "scene") return run_scene(argv[2]);
     if (mode == "oracle" && argc == 4)

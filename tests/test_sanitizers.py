@@ -75,6 +75,28 @@ def test_bvh_builder(san, kind):
     assert f"bvh {n} triangles" in out
 
 
+@pytest.mark.parametrize("kind", ["random", "coincident", "nonfinite", "odd", "big"])
+def test_sphere_chunk_builder(san, kind):
+    """The packet kernel's spatial sphere chunks (rt_bvh.cpp build_sphere_chunks): a permutation
+    and per-chunk bounding spheres that contain their members, under ASan/UBSan."""
+    exe, d = san
+    rng = np.random.default_rng(abs(hash(kind)) % 2 ** 32)
+    n = {"random": 256, "coincident": 130, "nonfinite": 200, "odd": 65, "big": 5000}[kind]
+    c = rng.uniform(-20, 20, (n, 3))
+    r = rng.uniform(0.1, 3.0, n)
+    if kind == "coincident":   # identical centres (ties in every split)
+        c[:] = c[0]
+    if kind == "nonfinite":    # NaN / inf centres and radii: their chunks are never culled
+        c[5, 0] = np.nan
+        c[77, 2] = np.inf
+        r[150] = np.inf
+    rec = np.concatenate([c, (r * r)[:, None]], axis=1).astype(np.float64)
+    path = d / f"sph_{kind}.bin"
+    rec.tofile(path)
+    out = _run(exe, "chunks", path, n)
+    assert f"chunks {n} spheres" in out
+
+
 MALFORMED_OBJ = [
     "v 1 2 3\nv 4 5 6\nv 7 8 9\nf 1 2 3\n",
     "v 1 2 3\nf 1 2 3\n",                         # indices past the vertex list
