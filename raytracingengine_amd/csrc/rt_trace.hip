@@ -1,7 +1,7 @@
 // rt_trace.hip — the per-pixel FP64 trace kernels for gfx950 (MI355X).
 //
-// One thread per pixel (per AA sample loop), one wave = 64 contiguous pixels of a row, one
-// 256-thread workgroup = a 64×4 tile.  Sphere/plane/light records are staged into LDS once per
+// One thread per pixel (per AA sample loop), one wave = an 8×8 tile, one 256-thread workgroup
+// = an 8×32 tile.  Sphere/plane/light records are staged into LDS once per
 // workgroup and read as wave-uniform broadcasts; materials are read from HBM (L2) for the
 // winning primitive only.  Geometry is evaluated in IEEE binary64 with the reference's
 // operation order (no FMA contraction), so radiance is bit-identical to
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParam
             t += __shfl_xor(t, off, 64);
             s += __shfl_xor(s, off, 64);
         }
-        if ((threadIdx.x & 63) == 0) {
+        if ((tid & 63) == 0) {
             atomicAdd(P.counters + 0, static_cast<unsigned long long>(t));
             atomicAdd(P.counters + 1, static_cast<unsigned long long>(s));
         }
