@@ -54,6 +54,17 @@ __device__ __forceinline__ void level_range(const WfArena& A, int level, uint32_
     n = base >= A.cap ? 0u : min(want, A.cap - base);
 }
 
+// Level 0's lanes take the camera rays in 8×8 pixel tiles (row-major over the tiles) when both
+// sides are multiples of 8, so each wave — and, through the wave-ordered child append, each
+// wave of the deeper levels — holds one coherent tile.  Node ids stay row-major (id = root).
+__device__ __forceinline__ uint32_t wf_tile_order(const TraceParams& P, uint32_t i, uint32_t aa) {
+    if ((P.width & 7u) != 0 || (P.rows & 7u) != 0) return i;
+    const uint32_t t = i / aa, s = i - t * aa;
+    const uint32_t tile = t >> 6, w = t & 63u, tiles_x = P.width >> 3;
+    const uint32_t x = (tile % tiles_x) * 8u + (w & 7u), yl = (tile / tiles_x) * 8u + (w >> 3);
+    return (yl * P.width + x) * aa + s;
+}
+
 // level kernels: 2 waves/SIMD, 3 in the lean build (213 → 168 VGPRs: glass 1.58 → 1.54 ms)
 #ifdef RT_LEAN_GENERIC
 constexpr int kWfLevelWaves = 3;
@@ -78,7 +89,7 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
          i0 += gridDim.x * kWfThreads) {
         const uint32_t i = i0 + lane;
         const bool active = i < n;
-        const uint32_t id = base + (active ? i : 0u);
+        const uint32_t id = base + (active ? (level == 0 ? wf_tile_order(P, i, aa) : i) : 0u);
         uint32_t root;
         d3 o, d;
         if (level == 0) {
