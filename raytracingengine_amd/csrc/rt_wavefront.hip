@@ -12,7 +12,8 @@
 //                    the child rays are appended to level k+1 with one atomic per wave;
 //   fold kernel k    deepest level first, value = (local + refraction_child·fw) +
 //                    reflection_child·rw — the reference's accumulation order (Scene.h:176-195);
-//   final kernel     the AA average of each pixel's root values, stored like GeneratePixelAt.
+//   final kernel     the roots' fold, the AA average of each pixel's root values, stored like
+//                    GeneratePixelAt.
 //
 // Every ray is computed by the same instructions as in the per-pixel kernels and every node is
 // folded in the reference's order, so the image is bit-identical to them.  Node/ray records live
@@ -193,7 +194,8 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold_kernel(WfArena A, int leve
     }
 }
 
-// GeneratePixelAt (Scene.h:283-304): accumulated / samples, then the outputs
+// GeneratePixelAt (Scene.h:283-304): each root folded with its children, accumulated / samples,
+// then the outputs
 __global__ __launch_bounds__(kWfThreads) void wf_final_kernel(TraceParams P, WfArena A) {
     const size_t npx = static_cast<size_t>(P.rows) * P.width;
     const size_t p = static_cast<size_t>(blockIdx.x) * kWfThreads + threadIdx.x;
@@ -205,7 +207,12 @@ __global__ __launch_bounds__(kWfThreads) void wf_final_kernel(TraceParams P, WfA
     int samples = 0;
     for (size_t s = 0; s < aa; ++s) {
         const size_t id = p * aa + s;
-        acc = acc + mk(A.val[id], A.val[A.cap + id], A.val[2 * A.cap + id]);
+        // the root's fold (wf_fold_kernel for level 0, same operations) done here
+        d3 v = mk(A.val[id], A.val[A.cap + id], A.val[2 * A.cap + id]);
+        const int32_t cf = A.child[id], cr = A.child[A.cap + id];
+        if (cf >= 0) v = v + mk(A.val[cf], A.val[A.cap + cf], A.val[2 * A.cap + cf]) * A.fw[id];
+        if (cr >= 0) v = v + mk(A.val[cr], A.val[A.cap + cr], A.val[2 * A.cap + cr]) * A.rw[id];
+        acc = acc + v;
         samples += 1;
     }
     const d3 v = samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0);
@@ -218,8 +225,18 @@ hipError_t launch_levels(const TraceParams& p, const WfArena& A, size_t lds_byte
     const int max_level = p.max_rec > 0 ? p.max_rec : 0;
     // level 0 exactly covers the roots; deeper levels are persistent grids over the arena
     const uint32_t g0 = static_cast<uint32_t>((A.n0 + kWfThreads - 1) / kWfThreads);
+    // Deeper levels: one resident round of workgroups (kWfLevelWaves per CU for the level
+    // kernels, 8 for the folds), not more — a level holds far fewer rays than the frame has
+    // pixels, and surplus workgroups that find nothing to do still cost their dispatch.
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+        cus = 256;
+    const size_t rounds = (A.cap_r + kWfThreads - 1) / kWfThreads;
     const uint32_t gk = static_cast<uint32_t>(
-        std::min<size_t>(4096, (A.cap_r + kWfThreads - 1) / kWfThreads));
+        std::min<size_t>(static_cast<size_t>(cus) * kWfLevelWaves, rounds));
+    const uint32_t gf = static_cast<uint32_t>(std::min<size_t>(static_cast<size_t>(cus) * 8, rounds));
     const size_t lds = LDS ? lds_bytes : 0;
     if (g0 > 0)
         hipLaunchKernelGGL((wf_level_kernel<TREE, LDS>), dim3(g0), dim3(kWfThreads), lds, stream,
@@ -227,10 +244,8 @@ hipError_t launch_levels(const TraceParams& p, const WfArena& A, size_t lds_byte
     for (int k = 1; k <= max_level && gk > 0; ++k)
         hipLaunchKernelGGL((wf_level_kernel<TREE, LDS>), dim3(gk), dim3(kWfThreads), lds, stream,
                            p, A, k);
-    for (int k = max_level - 1; k >= 1 && gk > 0; --k)
-        hipLaunchKernelGGL(wf_fold_kernel, dim3(gk), dim3(kWfThreads), 0, stream, A, k);
-    if (g0 > 0 && max_level >= 1)
-        hipLaunchKernelGGL(wf_fold_kernel, dim3(g0), dim3(kWfThreads), 0, stream, A, 0);
+    for (int k = max_level - 1; k >= 1 && gf > 0; --k)
+        hipLaunchKernelGGL(wf_fold_kernel, dim3(gf), dim3(kWfThreads), 0, stream, A, k);
     const size_t npx = static_cast<size_t>(p.rows) * p.width;
     if (npx > 0)
         hipLaunchKernelGGL(wf_final_kernel, dim3(static_cast<uint32_t>((npx + kWfThreads - 1) /
