@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <cmath>
 #include <cstdlib>
@@ -206,6 +207,48 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
 // positions are remembered.  Past kMaxPkImages cached cameras the kernel forms it in LDS.
 constexpr size_t kMaxPkImages = 16;
 constexpr size_t kMaxPkSeen = 16;
+// A camera without a cached image gets a publish slot instead: the launch's first workgroup
+// forms the image and hands it to the later ones through {epoch, word} granules (rt_packet.hip).
+// Slots rotate so that launches in flight on other streams keep theirs; a slot overwritten by a
+// later launch only fails its tags (the workgroup then forms the image itself).  Images above
+// kPkPubMaxWords 32-bit words (4 KiB, about 32 spheres) are formed per workgroup: reading twice
+// their size in granules costs as much as forming them (moving camera, MI355X: C2's 1.9 KiB
+// image 54.1 -> 50.8 us; C3's 14.3 KiB 555 -> 555 us; C5's 6.5 KiB 522 -> 530 us).
+constexpr size_t kPkPubSlots = 8;
+constexpr size_t kPkPubMaxWords = 1024;
+// Epochs are unique across the process (not per scene): a slot whose memory held another
+// scene's granules (a freed and re-allocated buffer) can never match a later launch's tags.
+std::atomic<uint32_t> g_pk_epoch{0};
+rt_status packet_publish_slot(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
+    const size_t words = packet_lds_bytes(p.ns, p.np, p.nl) / 4;
+    static const bool off = [] {  // RTAMD_PK_PUB=0: every workgroup forms it (A/B runs)
+        const char* e = std::getenv("RTAMD_PK_PUB");
+        return e && std::atoi(e) == 0;
+    }();
+    if (off || words > kPkPubMaxWords) return RT_OK;
+    const size_t slot = kPkPubMaxWords * sizeof(unsigned long long);
+    if (!sc->pk_pub.ptr) {
+        // zeroed (epoch 0 is never used) and complete before any stream's launch reads it
+        RT_HIP(sc->pk_pub.ensure(kPkPubSlots * slot));
+        RT_HIP(hipMemsetAsync(sc->pk_pub.ptr, 0, kPkPubSlots * slot, ctx->stream));
+        RT_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    uint32_t ep = ++g_pk_epoch;
+    if (ep == 0) ep = ++g_pk_epoch;
+    p.pk_epoch = ep;
+    // the first resident round: 256 CUs x 10 workgroups of 128 threads (20 waves per CU)
+    static const long first_env = [] {
+        const char* e = std::getenv("RTAMD_PK_PUB_FIRST");
+        return e ? std::atol(e) : -1L;
+    }();
+    int cus = 0;
+    RT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    p.pk_pub_first = first_env >= 0 ? static_cast<uint32_t>(first_env)
+                                    : static_cast<uint32_t>(cus > 0 ? cus : 256) * 10u;
+    p.pk_pub = reinterpret_cast<unsigned long long*>(static_cast<char*>(sc->pk_pub.ptr) +
+                                                     (ep % kPkPubSlots) * slot);
+    return RT_OK;
+}
 rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
     for (auto& im : sc->pk_images) {
         if (std::memcmp(im.cam, p.cam_pos, sizeof im.cam) != 0) continue;
@@ -225,9 +268,9 @@ rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
     if (it == seen.end()) {  // first sighting: remember it, no setup launch
         if (seen.size() >= kMaxPkSeen) seen.erase(seen.begin());
         seen.push_back({p.cam_pos[0], p.cam_pos[1], p.cam_pos[2]});
-        return RT_OK;
+        return packet_publish_slot(ctx, sc, p);
     }
-    if (sc->pk_images.size() >= kMaxPkImages) return RT_OK;
+    if (sc->pk_images.size() >= kMaxPkImages) return packet_publish_slot(ctx, sc, p);
     seen.erase(it);
     sc->pk_images.emplace_back();
     rt_scene::PkImage& im = sc->pk_images.back();
@@ -567,6 +610,7 @@ rt_status rt_scene_destroy(rt_scene* sc) {
     // the current one: wait for the whole device before freeing.
     (void)hipDeviceSynchronize();
     sc->buf.release();
+    sc->pk_pub.release();
     for (auto& im : sc->pk_images) {
         im.buf.release();
         if (im.ready) (void)hipEventDestroy(im.ready);

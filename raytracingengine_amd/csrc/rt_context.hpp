@@ -104,6 +104,9 @@ struct rt_scene {
     };
     mutable std::vector<PkImage> pk_images;
     mutable std::vector<std::array<double, 3>> pk_seen;  // cameras rendered once, no image yet
+    // Cameras without an image: a ring of kPkPubSlots publish slots (rt_packet.hip, in-launch
+    // image hand-off), each launch tagged with its own epoch; zeroed once at allocation.
+    mutable rtamd::DeviceBuffer pk_pub;
 };
 
 namespace rtamd {

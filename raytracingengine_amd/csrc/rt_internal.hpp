@@ -73,6 +73,11 @@ struct TraceParams {
     const double* bvh;       // triangle BVH nodes (rt_bvh.cpp), or null: test every triangle
     const int32_t* bvh_tri;  // triangle ids in leaf order
     const double* pk_image;  // packet kernel: LDS image of this scene + camera, or null
+    // packet kernel, camera without a cached image: the slot the launch's first workgroup
+    // publishes its image to ({epoch, word} granules, one per 32-bit image word), or null
+    unsigned long long* pk_pub;
+    uint32_t pk_epoch;       // this launch's tag (never 0)
+    uint32_t pk_pub_first;   // workgroups below this linear index form the image themselves
     // packet kernel, ns >= kSphChunkMin: spatial sphere order and chunk bounds (build_sphere_chunks)
     const int32_t* sph_perm;
     const double* sph_bnd;

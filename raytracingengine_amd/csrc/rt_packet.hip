@@ -929,15 +929,52 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, FEAT == kFeatTris ? RT_PACKET
     double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
     const int32_t* s_orig = reinterpret_cast<const int32_t*>(s_pln + 4 * np);
     const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    constexpr int kThreads = 64 * kWgWavesX * WGY;
     if (P.pk_image) {  // the image of this scene and camera, formed once (packet_image_kernel)
         const float4* src = reinterpret_cast<const float4*>(P.pk_image);
         float4* dst = reinterpret_cast<float4*>(smem);
         const int nv = static_cast<int>(pk_image_bytes(ns, np, nl) / 16);
-        for (int i = tid; i < nv; i += 64 * kWgWavesX * WGY) dst[i] = src[i];
+        for (int i = tid; i < nv; i += kThreads) dst[i] = src[i];
+        __syncthreads();
+    } else if (P.pk_pub) {
+        // A camera without a cached image: the launch's first workgroup forms the image and
+        // publishes it as {epoch, word} granules (8-byte agent-scope atomic stores, written
+        // through to memory: the tag travels with its word, so no flag and no fence).  The
+        // workgroups of the first resident round (linear index < pk_pub_first) form their own
+        // and never read the slot, so no XCD's L2 holds a line of it from before the publish;
+        // a later workgroup reads the granules with plain 16-byte loads and copies them when
+        // every tag is this launch's epoch.  A granule with this epoch can only hold this
+        // launch's word, so a stale or half-published slot just means "form it".
+        uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
+        const int nw = static_cast<int>(pk_image_bytes(ns, np, nl) / 4);  // a multiple of 4
+        const uint32_t ep = P.pk_epoch;
+        const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
+        bool have = false;
+        if (wg >= P.pk_pub_first) {
+            const ulonglong2* src = reinterpret_cast<const ulonglong2*>(P.pk_pub);
+            int ok = 1;
+            for (int i = tid; i < nw / 2; i += kThreads) {
+                const ulonglong2 g = src[i];
+                ok &= static_cast<uint32_t>(g.x >> 32) == ep && static_cast<uint32_t>(g.y >> 32) == ep;
+                dst[2 * i] = static_cast<uint32_t>(g.x);
+                dst[2 * i + 1] = static_cast<uint32_t>(g.y);
+            }
+            have = __syncthreads_and(ok) != 0;
+        }
+        if (!have) {
+            pk_build_image(P, smem, tid, kThreads);
+            __syncthreads();
+            if (wg == 0) {
+                const unsigned long long tag = static_cast<unsigned long long>(ep) << 32;
+                for (int i = tid; i < nw; i += kThreads)
+                    __hip_atomic_store(P.pk_pub + i, tag | dst[i], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     } else {
-        pk_build_image(P, smem, tid, 64 * kWgWavesX * WGY);
+        pk_build_image(P, smem, tid, kThreads);
+        __syncthreads();
     }
-    __syncthreads();
 
     PacketScene S;
     S.sph = s_sph;

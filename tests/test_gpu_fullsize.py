@@ -132,3 +132,62 @@ def test_full_frame_pow_scenes_vs_reference_subsample(ctx, golden, name):
                 assert _sha(out["ldr"]) == info["ldr_sha256"]["aces"]
     finally:
         ds.close()
+
+
+def _moved(sc, k):
+    import copy
+    import dataclasses
+    out = copy.copy(sc)
+    x, y, z = sc.camera.position
+    out.camera = dataclasses.replace(sc.camera, position=(x + 0.35 * k - 1.5, y + 0.2 * k - 0.5,
+                                                          z - 0.25 * k))
+    return out
+
+
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_full_frame_moving_camera_publish_slots(ctx, oracle, name):
+    """A camera that moves every frame (the bench's `moving_camera` field): no cached packet
+    image, so each launch's first workgroup forms the image and publishes it to a tagged slot
+    that the later workgroups copy (rt_packet.hip, rt_capi.cpp packet_publish_slot).  At 1080p
+    a launch has ~16k workgroups, so most of them take the copy.  10 cameras rotate through the
+    8 slots (slots 1 and 2 hold an older epoch's granules when reused), rendered back to back
+    without a synchronisation, every frame bit-identical to the oracle's HDR and bytes.  C3's
+    image is above the hand-off's size limit: every workgroup forms it (the control)."""
+    base = make_config(name, 1920, 1080)
+    ds = ctx.scene(base)
+    try:
+        outs = []
+        for k in range(10):
+            ds.camera = _moved(base, k).camera.to_struct()
+            outs.append(ds.render(hdr64=True, tonemap=1))
+        for k in (0, 1, 8, 9):
+            ref = oracle.render(_moved(base, k))[0]
+            assert np.array_equal(outs[k]["hdr64"], ref), (name, k)
+            assert np.array_equal(outs[k]["ldr"], oracle.tonemap(ref, 1).reshape(outs[k]["ldr"].shape))
+    finally:
+        ds.close()
+
+
+def test_moving_camera_on_two_streams(ctx):
+    """Moving-camera launches in flight on two streams at once, each with its own publish slot:
+    every frame equals the synchronous render of its camera."""
+    import torch
+    base = make_config("c2", 1920, 1080)
+    n = 1920 * 1080 * 3
+    ds = ctx.scene(base)
+    try:
+        bufs = [torch.empty(n, dtype=torch.float64, device="cuda") for _ in range(12)]
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        for k, buf in enumerate(bufs):
+            ctx.set_stream(streams[k % 2].cuda_stream)
+            ds.camera = _moved(base, 20 + k).camera.to_struct()
+            ds.render_device(buf.data_ptr(), None, None, capi.default_opts())
+        for s in streams:
+            s.synchronize()
+        ctx.set_stream(None)
+        for k in (0, 1, 10, 11):
+            ds.camera = _moved(base, 20 + k).camera.to_struct()
+            ref = ds.render(hdr64=True)["hdr64"].reshape(-1)
+            assert np.array_equal(bufs[k].cpu().numpy(), ref), k
+    finally:
+        ds.close()
