@@ -495,7 +495,8 @@ def main(argv=None):
                 "kernel_ms_per_launch": round(mv["region_ms"], 6),
                 "value": round(mv["rays"] * steps_x / mv["elapsed"] / 1e6, 3),
                 "note": "camera x moved by 1e-7 every frame: the per-camera packet image is "
-                        "never reused; rays counted at the first position"}
+                        "never reused (each launch's first workgroup forms it and hands it to "
+                        "the later ones, DESIGN §4); rays counted at the first position"}
             if args.inflight > 1:
                 el = pipelined_frames(R, sc, steps_x, args.warmup, args.inflight, tonemap)
                 line["pipelined"] = {
