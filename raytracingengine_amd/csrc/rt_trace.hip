@@ -18,6 +18,9 @@
 #pragma clang fp contract(off)
 
 namespace rtamd {
+#ifndef RT_CHAIN_NOSPH_WAVES
+#define RT_CHAIN_NOSPH_WAVES 3
+#endif
 #ifdef RT_LEAN_GENERIC
 // rt_trace_lean.hip: the per-pixel kernels again, without the triangle / BVH and area-light code
 // (rt_trace_common.hpp), for scenes that have neither: fewer registers, C1 / mirror ~5 % faster.
@@ -26,7 +29,10 @@ namespace lean {
 
 // MINW: minimum waves per SIMD the register budget is compiled for; SINGLE: one sample per pixel
 // (AA = 1: no sample loop, no accumulator live across the trace).
-template <int PATH, bool COUNT, bool LDS, int MINW = 2, bool SINGLE = false>
+// NOSPH: the scene has no spheres (C1, the reference's own box of planes): the sphere loops and
+// the sphere shading code compile away (AA = 1 chain: 80 -> 48 B/lane of spills at 3 waves/SIMD,
+// C1 489 -> 453 us on MI355X; at 4 waves it spills 224 B/lane and takes 808 us, at 5 1256 us).
+template <int PATH, bool COUNT, bool LDS, int MINW = 2, bool SINGLE = false, bool NOSPH = false>
 __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParams P) {
     extern __shared__ double smem[];
     const int tid = threadIdx.y * kTileW + threadIdx.x;
@@ -45,7 +51,8 @@ __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParam
         }
         if (!__syncthreads_or(run)) return;
     }
-    const SceneView S = stage_scene<LDS>(P, smem, tid, kTileW * kTileH);
+    SceneView S = stage_scene<LDS>(P, smem, tid, kTileW * kTileH);
+    if constexpr (NOSPH) S.ns = 0;  // the launcher checked P.ns == 0
     if (run) {
         const uint32_t y = image_row(P, yl);
         const uint64_t pix = static_cast<uint64_t>(y) * P.width + x;
@@ -83,23 +90,23 @@ __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParam
     }
 }
 
-template <int PATH, bool COUNT, bool LDS, int MINW, bool SINGLE>
+template <int PATH, bool COUNT, bool LDS, int MINW, bool SINGLE, bool NOSPH = false>
 static hipError_t launch_one(const TraceParams& p, size_t lds_bytes, hipStream_t stream) {
     const dim3 block(kTileW, kTileH);
     const dim3 grid((p.width + kTileW - 1) / kTileW, (p.rows + kTileH - 1) / kTileH);
-    hipLaunchKernelGGL((trace_kernel<PATH, COUNT, LDS, MINW, SINGLE>), grid, block,
+    hipLaunchKernelGGL((trace_kernel<PATH, COUNT, LDS, MINW, SINGLE, NOSPH>), grid, block,
                        LDS ? lds_bytes : 0, stream, p);
     return hipGetLastError();
 }
 
-template <int PATH, int MINW, bool SINGLE>
+template <int PATH, int MINW, bool SINGLE, bool NOSPH = false>
 static hipError_t launch_lds(const TraceParams& p, bool count, bool lds, size_t lds_bytes,
                              hipStream_t stream) {
     if (count)
-        return lds ? launch_one<PATH, true, true, MINW, SINGLE>(p, lds_bytes, stream)
-                   : launch_one<PATH, true, false, MINW, SINGLE>(p, lds_bytes, stream);
-    return lds ? launch_one<PATH, false, true, MINW, SINGLE>(p, lds_bytes, stream)
-               : launch_one<PATH, false, false, MINW, SINGLE>(p, lds_bytes, stream);
+        return lds ? launch_one<PATH, true, true, MINW, SINGLE, NOSPH>(p, lds_bytes, stream)
+                   : launch_one<PATH, true, false, MINW, SINGLE, NOSPH>(p, lds_bytes, stream);
+    return lds ? launch_one<PATH, false, true, MINW, SINGLE, NOSPH>(p, lds_bytes, stream)
+               : launch_one<PATH, false, false, MINW, SINGLE, NOSPH>(p, lds_bytes, stream);
 }
 
 template <int PATH>
@@ -111,6 +118,8 @@ static hipError_t launch_path(const TraceParams& p, bool count, bool lds, size_t
     // 2189 -> 1684 us on MI355X; 4 waves spills 320 B/lane and loses (C1 900 us).  AA = 1 takes
     // the single-sample instantiation (80 instead of 144 B/lane of spills).
     if constexpr (PATH == kPathChain) {
+        if (p.ns == 0 && p.aa == 1 && !p.redo)
+            return launch_lds<PATH, RT_CHAIN_NOSPH_WAVES, true, true>(p, count, lds, lds_bytes, stream);
         if (p.aa == 1 && !p.redo) return launch_lds<PATH, 3, true>(p, count, lds, lds_bytes, stream);
         return launch_lds<PATH, 3, false>(p, count, lds, lds_bytes, stream);
     } else
