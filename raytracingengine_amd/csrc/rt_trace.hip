@@ -121,6 +121,7 @@ static hipError_t launch_path(const TraceParams& p, bool count, bool lds, size_t
         if (p.ns == 0 && p.aa == 1 && !p.redo)
             return launch_lds<PATH, RT_CHAIN_NOSPH_WAVES, true, true>(p, count, lds, lds_bytes, stream);
         if (p.aa == 1 && !p.redo) return launch_lds<PATH, 3, true>(p, count, lds, lds_bytes, stream);
+        if (p.ns == 0 && !p.redo) return launch_lds<PATH, 3, false, true>(p, count, lds, lds_bytes, stream);
         return launch_lds<PATH, 3, false>(p, count, lds, lds_bytes, stream);
     } else
 #endif

@@ -270,7 +270,7 @@ def test_deterministic(ctx):
     assert np.array_equal(a["hdr64"], b["hdr64"])
 
 
-@pytest.mark.parametrize("name,aa", [("c2", 4), ("mirror", 3), ("glass", 2)])
+@pytest.mark.parametrize("name,aa", [("c2", 4), ("mirror", 3), ("glass", 2), ("c1", 4)])
 def test_antialiasing_vs_oracle(ctx, oracle, name, aa):
     """AA>1 uses the build-defined counter RNG (the reference's is unseeded); same RNG on
     both sides gives identical jitter."""

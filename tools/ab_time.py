@@ -8,7 +8,7 @@ from raytracingengine_amd.configs import make_config
 ctx = capi.Context(0)
 s = torch.cuda.Stream(); ctx.set_stream(s.cuda_stream)
 for name in sys.argv[1:] or ["c2"]:
-    sc = make_config(name)
+    sc = make_config("c1", aa=32) if name == "c1_aa32" else make_config(name)
     ds = ctx.scene(sc)
     W, H = sc.camera.width, sc.camera.height
     hdr = torch.empty(W * H * 3, dtype=torch.float64, device="cuda")
