@@ -65,6 +65,10 @@ constexpr int kFeatTris = 4;    // triangles / models
 constexpr int kFeatJodie = 8;   // Reinhard-Jodie fused tonemap (log/pow)
 constexpr int kFeatPlanes = 16; // ≥ 3 planes: shadow packets also cull planes (cull_capsule)
 constexpr int kFeatAll = 31;
+// with kFeatArea only: no planes and no point lights (C5: spheres lit by the area light), so the
+// plane and point-light code compiles away; the single-sample instantiation then runs at 6
+// waves/SIMD (80 VGPRs): C5 508 -> 490 us at 5 waves, -> 482 us at 6 (MI355X)
+constexpr int kFeatNoPL = 32;
 
 // Waves per SIMD the lean variants are compiled for (4 = at most 128 VGPRs).
 #ifndef RT_PACKET_LEAN_WAVES
@@ -916,10 +920,12 @@ __device__ __forceinline__ void pk_build_image(const TraceParams& P, double* img
 }
 
 template <int MAXC, int FEAT, bool COUNT, bool MULTI, int WGY>  // MULTI = false: one sample (AA = 1)
-__global__ __launch_bounds__(64 * kWgWavesX * WGY, FEAT == kFeatTris ? RT_PACKET_TRIS_WAVES : (((FEAT == 0 || FEAT == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1)) void packet_direct_kernel(TraceParams P) {
+__global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNoPL) && !MULTI && !COUNT) ? 6 : FEAT == kFeatTris ? RT_PACKET_TRIS_WAVES : (((FEAT == 0 || (FEAT & ~kFeatNoPL) == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1)) void packet_direct_kernel(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
-    const int ns = P.ns, np = P.np, nl = P.nl, nb = pk_chunk_bounds(ns), nsb = ns + nb;
+    constexpr bool kNoPL = (FEAT & kFeatNoPL) != 0;  // the launcher checked P.np == P.nl == 0
+    const int ns = P.ns, np = kNoPL ? 0 : P.np, nl = kNoPL ? 0 : P.nl, nb = pk_chunk_bounds(ns),
+              nsb = ns + nb;
     double* s_sph = smem;                                         // 32·nsb bytes
     float* s_cone = reinterpret_cast<float*>(s_sph + kSphStride * nsb);  // 16-byte aligned
     double* s_rad = s_sph + (kSphStride + 4) * nsb;
@@ -1240,7 +1246,9 @@ static void launch_packet_variant(const TraceParams& p, bool count, size_t lds, 
 // variants keep).
 hipError_t launch_packet_area(const TraceParams& p, bool count, size_t lds, int chunks,
                               hipStream_t stream) {
-    if (chunks <= 1) launch_packet_variant<1, kFeatArea>(p, count, lds, stream);
+    if (p.np == 0 && p.nl == 0 && chunks <= 1)
+        launch_packet_variant<1, kFeatArea | kFeatNoPL>(p, count, lds, stream);
+    else if (chunks <= 1) launch_packet_variant<1, kFeatArea>(p, count, lds, stream);
     else if (chunks <= 4) launch_packet_variant<4, kFeatArea>(p, count, lds, stream);
     else launch_packet_variant<16, kFeatArea>(p, count, lds, stream);
     return hipGetLastError();
