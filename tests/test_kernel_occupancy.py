@@ -1,7 +1,7 @@
 """Register budgets of the built gfx950 kernels (CPU: reads the code objects' metadata).
 
 Occupancy is the lever measured most in DESIGN.md §4: the single-sample packet kernels run at
-5 waves/SIMD (≤ 96 VGPRs + AGPRs), the lean reflection-chain kernels at 3 (≤ 168: C1 -19 %,
+5 waves/SIMD (≤ 96 VGPRs + AGPRs; the area-only one at 6, ≤ 80), the lean reflection-chain kernels at 3 (≤ 168: C1 -19 %,
 mirror -23 % against 2) and the other generic / breadth-first trace kernels at 2 (≤ 256).
 An unrelated change once pushed the breadth-first level kernel into AGPRs and 1 wave/SIMD
 (glass +35 %); this pins the budgets on the objects `build()` produced."""
@@ -49,9 +49,12 @@ def test_packet_single_sample_kernels_run_at_5_waves():
     # packet_direct_kernel<MAXC, FEAT, COUNT=false, MULTI=false, WGY>, FEAT 0 (lean), 2 (area)
     # or 16 (plane cull)
     lean = {n: r for n, r in ks.items()
-            if re.search(r"packet_direct_kernelILi[14]ELi(0|2|16)ELb0ELb0E", n)}
-    assert len(lean) == 12, sorted(lean)
+            if re.search(r"packet_direct_kernelILi[14]ELi(0|2|16|34)ELb0ELb0E", n)}
+    assert len(lean) == 14, sorted(lean)
     assert all(_waves(r) >= 5 for r in lean.values()), lean
+    # the area-only variant (FEAT 34 = area light, no planes / point lights: C5) runs at 6
+    area_only = {n: r for n, r in lean.items() if "ELi34E" in n}
+    assert len(area_only) == 2 and all(_waves(r) >= 6 for r in area_only.values()), area_only
 
 
 @pytest.mark.parametrize("src", ["rt_trace.hip", "rt_trace_lean.hip", "rt_wavefront.hip"])
@@ -63,8 +66,9 @@ def test_generic_trace_kernels_run_at_2_waves(src):
 
 
 def test_lean_chain_kernels_run_at_3_waves():
-    """trace_kernel<PATH = chain, COUNT, LDS, MINW = 3, SINGLE> of rt_trace_lean.hip (C1, mirror)."""
+    """trace_kernel<PATH = chain, COUNT, LDS, MINW = 3, SINGLE, NOSPH> of rt_trace_lean.hip (C1,
+    mirror; NOSPH: the sphere-free instantiations C1 takes)."""
     ks = _kernels("rt_trace_lean.hip")
     chain = {n: r for n, r in ks.items() if re.search(r"trace_kernelILi1ELb[01]ELb[01]ELi3E", n)}
-    assert len(chain) == 8, sorted(ks)
+    assert len(chain) == 16, sorted(ks)
     assert all(_waves(r) >= 3 for r in chain.values()), chain
