@@ -290,6 +290,26 @@ rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
     return RT_OK;
 }
 
+// Whether a render of this TraceRay shape takes the breadth-first path, whose arena (ctx->wf,
+// ctx->wf_ctl) is one per context: refraction trees, and reflection chains when
+// RTAMD_WF_CHAIN=1 forces them there.
+bool uses_wavefront_arena(int path, int flags) {
+    if (flags & RT_FLAG_GENERIC_KERNEL) return false;
+    const char* wf_chain = std::getenv("RTAMD_WF_CHAIN");
+    return path == kPathTree || (path == kPathChain && wf_chain && std::atoi(wf_chain) == 1);
+}
+
+bool render_uses_context_scratch(const rt_scene* sc, const rt_render_opts* opts) {
+    rt_render_opts o;
+    if (opts) o = *opts;
+    else rt_render_opts_default(&o);
+    if (o.flags & RT_FLAG_COUNT_RAYS) return true;  // the context's counter buffer
+    int path = kPathDirect;
+    if (sc->any_transparent) path = kPathTree;
+    else if (!(sc->max_specular <= o.bias) && o.max_recursion >= 1) path = kPathChain;
+    return uses_wavefront_arena(path, o.flags);
+}
+
 rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
                          const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr) {
     TraceParams p;
@@ -341,10 +361,7 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
     // Reflection chains stay per pixel: measured 2-3x faster there (coherent, no stack), while
     // the glass tree renders 4.6x faster breadth-first.  RTAMD_WF_CHAIN=1 forces chains too.
     bool wavefront = false;
-    const char* wf_chain = std::getenv("RTAMD_WF_CHAIN");
-    const bool wf_path = path == kPathTree ||
-                         (path == kPathChain && wf_chain && std::atoi(wf_chain) == 1);
-    if (wf_path && !(flags & RT_FLAG_GENERIC_KERNEL)) {
+    if (uses_wavefront_arena(path, flags)) {
         const size_t n0 = static_cast<size_t>(rows) * p.width *
                           static_cast<size_t>(p.aa > 0 ? p.aa : 0);
         const char* env = std::getenv("RTAMD_WF_MB");
@@ -444,10 +461,10 @@ rt_status rt_context_destroy(rt_context* ctx) {
             (void)hipEventDestroy(ev.first);
             (void)hipEventDestroy(ev.second);
         }
+    leave_groups(ctx);  // communicators of any group this context is in go first
     for (DeviceBuffer* b : {&ctx->out64, &ctx->out32, &ctx->ldr, &ctx->tm_in, &ctx->tm_out,
                             &ctx->dbg, &ctx->rays, &ctx->counters, &ctx->wf, &ctx->wf_ctl})
         b->release();
-    release_group(ctx);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return RT_OK;

@@ -75,6 +75,8 @@ struct rt_context {
     // context led (rt_multi.cpp); destroyed with the context
     std::vector<rt_context*> group_ctxs;
     std::vector<rt_comm*> group_comms;
+    // the contexts whose cached group includes this one (released when this one is destroyed)
+    std::vector<rt_context*> group_roots;
 };
 
 struct rt_scene {
@@ -119,9 +121,15 @@ rt_status validate_camera(const rt_camera* cam);
 // device outputs in the packed row order of opts.  The caller holds a DeviceGuard.
 rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
                          const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr);
+// Whether a render uses scratch the context holds once (the breadth-first TraceRay arena, the
+// ray counters): frames on different streams that do must not overlap (rt_queue.cpp).
+bool uses_wavefront_arena(int path, int flags);
+bool render_uses_context_scratch(const rt_scene* sc, const rt_render_opts* opts);
 // Adds the elapsed time of completed RT_FLAG_TIME_KERNEL event pairs to the context totals.
 rt_status harvest_events(rt_context* ctx, bool all);
 // rt_multi.cpp: releases the communicators rt_render_multi cached in ctx.
 void release_group(rt_context* ctx);
+// rt_multi.cpp: releases ctx's own group and every group that includes ctx (context teardown).
+void leave_groups(rt_context* ctx);
 
 }  // namespace rtamd

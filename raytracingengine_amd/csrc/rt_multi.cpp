@@ -374,12 +374,18 @@ rt_status render_multi_rccl(rt_context* const* ctxs, rt_scene* const* scenes, in
         if (st != RT_OK) return st;
         root->group_ctxs.assign(ctxs, ctxs + n);
         root->group_comms = comms;
+        // every member knows the group it is in, so destroying any of them first releases it
+        for (int i = 1; i < n; ++i) ctxs[i]->group_roots.push_back(root);
     }
     for (int i = 0; i < n; ++i) root->group_comms[i]->ctx = ctxs[i];
     rt_render_opts o;
     if (opts) o = *opts;
     else rt_render_opts_default(&o);
     if (stats) o.flags |= RT_FLAG_COUNT_RAYS;
+    // the device-to-host copies below run on root->stream: a pipelined frame would gather and
+    // assemble on the communicators' own streams, unordered with them (one-shot host frames
+    // gain nothing from the pipeline anyway)
+    o.flags &= ~RT_FLAG_PIPELINE;
     if (stats)
         for (int i = 0; i < n; ++i) {
             DeviceGuard g(ctxs[i]->device);
@@ -472,8 +478,22 @@ namespace rtamd {
 
 void release_group(rt_context* ctx) {
     for (rt_comm* c : ctx->group_comms) rt_comm_destroy(c);
+    for (rt_context* m : ctx->group_ctxs) {
+        if (m == ctx) continue;
+        auto& roots = m->group_roots;
+        roots.erase(std::remove(roots.begin(), roots.end(), ctx), roots.end());
+    }
     ctx->group_comms.clear();
     ctx->group_ctxs.clear();
+}
+
+void leave_groups(rt_context* ctx) {
+    // the groups other contexts lead that include ctx: released before ctx goes away (their
+    // communicators hold raw pointers to it); release_group edits ctx->group_roots, so copy
+    const std::vector<rt_context*> roots = ctx->group_roots;
+    for (rt_context* r : roots) release_group(r);
+    ctx->group_roots.clear();
+    release_group(ctx);
 }
 
 }  // namespace rtamd
@@ -560,8 +580,10 @@ rt_status rt_comm_create_all(rt_context* const* ctxs, int n, rt_comm** out) {
 rt_status rt_comm_destroy(rt_comm* c) {
     if (!c) return RT_OK;
     DeviceGuard g(c->device);
-    if (c->ctx && c->ctx->stream) (void)hipStreamSynchronize(c->ctx->stream);
-    if (c->gstream) (void)hipStreamSynchronize(c->gstream);
+    // Renders into this comm's send buffers run on its context's stream, which may be any
+    // stream (rt_context_set_stream) of a context that may already be gone: wait for the whole
+    // device instead of dereferencing c->ctx.
+    (void)hipDeviceSynchronize();
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
     for (auto* v : {&c->pending, &c->spare})
         for (auto& ev : *v)

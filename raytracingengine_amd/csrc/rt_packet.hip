@@ -948,22 +948,25 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
         // through to memory: the tag travels with its word, so no flag and no fence).  The
         // workgroups of the first resident round (linear index < pk_pub_first) form their own
         // and never read the slot, so no XCD's L2 holds a line of it from before the publish;
-        // a later workgroup reads the granules with plain 16-byte loads and copies them when
-        // every tag is this launch's epoch.  A granule with this epoch can only hold this
-        // launch's word, so a stale or half-published slot just means "form it".
+        // a later workgroup reads the granules with relaxed agent-scope 8-byte atomic loads
+        // (each {epoch, word} read whole, as written) and copies them when every tag is this
+        // launch's epoch.  A granule with this epoch can only hold this launch's word, so a
+        // stale or half-published slot just means "form it".
         uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
         const int nw = static_cast<int>(pk_image_bytes(ns, np, nl) / 4);  // a multiple of 4
         const uint32_t ep = P.pk_epoch;
         const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
         bool have = false;
         if (wg >= P.pk_pub_first) {
-            const ulonglong2* src = reinterpret_cast<const ulonglong2*>(P.pk_pub);
             int ok = 1;
             for (int i = tid; i < nw / 2; i += kThreads) {
-                const ulonglong2 g = src[i];
-                ok &= static_cast<uint32_t>(g.x >> 32) == ep && static_cast<uint32_t>(g.y >> 32) == ep;
-                dst[2 * i] = static_cast<uint32_t>(g.x);
-                dst[2 * i + 1] = static_cast<uint32_t>(g.y);
+                const unsigned long long gx = __hip_atomic_load(
+                    P.pk_pub + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long gy = __hip_atomic_load(
+                    P.pk_pub + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok &= static_cast<uint32_t>(gx >> 32) == ep && static_cast<uint32_t>(gy >> 32) == ep;
+                dst[2 * i] = static_cast<uint32_t>(gx);
+                dst[2 * i + 1] = static_cast<uint32_t>(gy);
             }
             have = __syncthreads_and(ok) != 0;
         }

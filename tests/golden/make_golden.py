@@ -7,7 +7,8 @@ and the reference's outputs for them.  The reference has no tests or fixtures of
 (SURVEY.md §4), so these are the pins of the oracle.
 
     python tests/golden/make_golden.py          # rewrites tests/golden/*.npz / *.json
-    python tests/golden/make_golden.py --full   # adds the full-size frames (FULL2_SCENES)
+    python tests/golden/make_golden.py --full [name ...]  # full-size frames (FULL2_SCENES)
+    python tests/golden/make_golden.py --oracle-full      # C5 (no reference semantics): oracle
 """
 from __future__ import annotations
 
@@ -218,11 +219,16 @@ def main():
 # (diagnostics on a mismatch; configs whose shading calls libm pow are compared on the subsample
 # within the pow tolerance).  LDR: sha256 of the bytes of tonemapAll() (7 operators) and
 # tonemap() (ACES) of the reference, RaytracingEngine.cpp:113-135,165-214.
-FULL2_SCENES = {"c2": 64, "c3": 1024, "c4": 4096, "mirror": 256, "glass": 256, "mesh": 256}
+# Round 3 adds c1 (the reference main() scene: BASELINE config 1 is "ACES tonemap ->
+# output.ppm", so its bytes are pinned for every operator too).
+FULL2_SCENES = {"c1": 64, "c2": 64, "c3": 1024, "c4": 4096, "mirror": 256, "glass": 256,
+                "mesh": 256}
 LDR_NAMES = REFAPP_NAMES + ["tonemap_aces"]
 
 
-def full_golden():
+def full_golden(names=None):
+    """``--full [name ...]``: (re)generate the full-size reference frames of `names` (default:
+    every FULL2_SCENES entry)."""
     if not po.ref_available():
         po.build()
     meta_path = os.path.join(HERE, "golden_meta.json")
@@ -232,6 +238,8 @@ def full_golden():
     full = dict(np.load(sub_path))
     with tempfile.TemporaryDirectory() as td:
         for name, stride in FULL2_SCENES.items():
+            if names and name not in names:
+                continue
             sc = make_config(name)
             img, ms, thr = po.ref_render(sc)
             flat = np.ascontiguousarray(img.reshape(-1, 3))
@@ -256,6 +264,31 @@ def full_golden():
         json.dump(meta, fh, indent=1, sort_keys=True)
 
 
+# BASELINE config 5 (the build-defined area light) has no reference semantics: its
+# full frame is pinned by the ORACLE (itself pinned bit for bit to the reference on every other
+# scene by tests/test_oracle_golden.py), and recorded as such ("source": "oracle").
+ORACLE_FULL_SCENES = ["c5"]
+
+
+def oracle_full_golden():
+    meta_path = os.path.join(HERE, "golden_meta.json")
+    with open(meta_path) as fh:
+        meta = json.load(fh)
+    for name in ORACLE_FULL_SCENES:
+        sc = make_config(name)
+        img, nt, ns = po.render(sc)
+        flat = np.ascontiguousarray(img.reshape(-1, 3))
+        meta["scenes"][f"{name}_full"] = {
+            "source": "oracle", "scene_sha256": scene_hash(sc), "width": sc.camera.width,
+            "height": sc.camera.height, "image_sha256": hashlib.sha256(flat.tobytes()).hexdigest(),
+            "trace_rays": nt, "shadow_rays": ns,
+            "ldr_sha256": {n: hashlib.sha256(po.tonemap(flat, i).tobytes()).hexdigest()
+                           for i, n in enumerate(REFAPP_NAMES)}}
+        print(name, "oracle", meta["scenes"][f"{name}_full"]["image_sha256"][:16], flush=True)
+    with open(meta_path, "w") as fh:
+        json.dump(meta, fh, indent=1, sort_keys=True)
+
+
 def obj_golden():
     """The reference application's LoadObject (tinyobjloader) on the OBJ fixtures: triangles as
     9 doubles each (oracle/_ref/ref_harness obj)."""
@@ -275,6 +308,8 @@ if __name__ == "__main__":
     elif "--obj" in sys.argv:
         obj_golden()
     elif "--full" in sys.argv:
-        full_golden()
+        full_golden([a for a in sys.argv[1:] if not a.startswith("--")])
+    elif "--oracle-full" in sys.argv:
+        oracle_full_golden()
     else:
         main()

@@ -89,3 +89,47 @@ def test_queue_rejects_bad_arguments(ctx):
         assert e.value.status == capi.RT_ERR_INVALID_ARG
     finally:
         q.close()
+
+
+@pytest.mark.parametrize("depth", [2, 3])
+def test_queue_refraction_tree_frames_share_the_arena_safely(ctx, depth):
+    """Glass (refraction trees) renders breadth-first through ONE arena per context: queued frames
+    of such scenes are serialised behind each other on any stream (rt_queue.cpp), interleaved
+    with packet frames (C2) that are not.  Every frame equals its synchronous render, including
+    a camera move between glass frames (different trees, different arena fill)."""
+    glass = ctx.scene(make_config("glass", 320, 180))
+    c2 = ctx.scene(make_config("c2", 320, 180))
+    q = capi.Queue(ctx, depth)
+    W, H = 320, 180
+    base = glass.camera["position"][0].copy()
+    cams = [base, base + (0.75, 0.5, 2.0)]
+    try:
+        ref_g = []
+        for c in cams:
+            glass.camera["position"][0] = c
+            ref_g.append(glass.render(hdr64=True, tonemap=1))
+        ref_c2 = c2.render(hdr64=True, tonemap=1)
+        n = 9
+        bufs = [(torch.empty(H * W * 3, dtype=torch.float64, device="cuda"),
+                 torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")) for _ in range(n)]
+        opts = capi.default_opts(tonemap=1)
+        kinds = []
+        for i in range(n):
+            h, l = bufs[i]
+            if i % 3 == 2:
+                kinds.append(None)
+                q.submit(c2, opts, h.data_ptr(), None, l.data_ptr())
+            else:
+                glass.camera["position"][0] = cams[i % 2]
+                kinds.append(i % 2)
+                q.submit(glass, opts, h.data_ptr(), None, l.data_ptr())
+        q.synchronize()
+        for i, (h, l) in enumerate(bufs):
+            r = ref_c2 if kinds[i] is None else ref_g[kinds[i]]
+            assert np.array_equal(h.cpu().numpy().reshape(H, W, 3), r["hdr64"]), i
+            assert np.array_equal(l.cpu().numpy().reshape(H, W, 3), r["ldr"]), i
+    finally:
+        glass.camera["position"][0] = base
+        q.close()
+        glass.close()
+        c2.close()
