@@ -215,7 +215,8 @@ rt_status rt_render(rt_context* ctx, const rt_scene* scene, const rt_camera* cam
  * at the whole image).  Contexts on distinct GPUs: the RCCL path — communicators over their
  * devices (ncclCommInitAll, created on first use and cached in ctxs[0] until the list changes),
  * rt_render_gather_all into ctxs[0]'s device, one device-to-host copy per output.  Contexts that
- * share a GPU (RCCL allows one rank per GPU): each context's rows are copied to their host rows.
+ * share a GPU (RCCL allows one rank per GPU): the same through rt_comm_create_local (the gather
+ * as device copies); RTAMD_MULTI_HOST=1 copies each context's rows straight to their host rows.
  * Stats, when requested, are summed over the contexts (kernel_ms: the slowest GPU's render). */
 rt_status rt_render_multi(rt_context* const* ctxs, rt_scene* const* scenes, int n,
                           const rt_camera* cam, const rt_render_opts* opts, double* hdr64_out,
@@ -252,6 +253,12 @@ rt_status rt_comm_create(rt_context* ctx, int nranks, int rank, const uint8_t* i
 /* n communicators, one per context, over n DISTINCT devices from one process (ncclCommInitAll);
  * comms_out[i] is rank i on ctxs[i]. */
 rt_status rt_comm_create_all(rt_context* const* ctxs, int n, rt_comm** comms_out);
+/* n communicators over n contexts of ONE process that may share a GPU (RCCL allows one rank per
+ * GPU): the same multi-rank frame — row plan, padded send buffers, rank 0's receive layout and
+ * assembly, the pipelined slots — with the gather done as device-to-device copies of every
+ * rank's packed rows into rank 0's receive buffer (what ncclGather delivers).  Driven only by
+ * rt_render_gather_all; rt_render_multi uses it for contexts that share a device. */
+rt_status rt_comm_create_local(rt_context* const* ctxs, int n, rt_comm** comms_out);
 rt_status rt_comm_destroy(rt_comm* comm);
 rt_status rt_comm_info(const rt_comm* comm, int* nranks, int* rank);
 /* Collective: every rank calls it with the same camera, opts and outputs (RT_OUT_* bits).  The
@@ -261,7 +268,8 @@ rt_status rt_comm_info(const rt_comm* comm, int* nranks, int* rank);
 rt_status rt_render_gather(rt_comm* comm, const rt_scene* scene, const rt_camera* cam,
                            const rt_render_opts* opts, int outputs, void* d_hdr64,
                            void* d_hdr32, void* d_ldr);
-/* The same from one process for every rank of an rt_comm_create_all (one ncclGroup). */
+/* The same from one process for every rank of an rt_comm_create_all (one ncclGroup) or of an
+ * rt_comm_create_local.  With n == 1 the rank renders straight into the framebuffers. */
 rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, int n,
                                const rt_camera* cam, const rt_render_opts* opts, int outputs,
                                void* d_hdr64, void* d_hdr32, void* d_ldr);

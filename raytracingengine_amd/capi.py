@@ -39,7 +39,7 @@ EXPORTED = [
     "rt_context_destroy", "rt_context_set_stream", "rt_context_synchronize", "rt_scene_create",
     "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
     "rt_render_multi", "rt_comm_unique_id", "rt_comm_create", "rt_comm_create_all",
-    "rt_comm_destroy", "rt_comm_info", "rt_render_gather", "rt_render_gather_all",
+    "rt_comm_create_local", "rt_comm_destroy", "rt_comm_info", "rt_render_gather", "rt_render_gather_all",
     "rt_comm_timing", "rt_comm_synchronize", "rt_debug_assemble_rows",
     "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
     "rt_debug_f64_ops", "rt_debug_vec_ops", "rt_queue_create", "rt_queue_destroy",
@@ -131,6 +131,7 @@ def load_library(path: str = LIB_PATH):
         "rt_comm_unique_id": [vp],
         "rt_comm_create": [vp, i32, i32, vp, vp],
         "rt_comm_create_all": [vp, i32, vp],
+        "rt_comm_create_local": [vp, i32, vp],
         "rt_comm_destroy": [vp],
         "rt_comm_info": [vp, vp, vp],
         "rt_render_gather": [vp, vp, vp, vp, i32, vp, vp, vp],
@@ -436,6 +437,16 @@ class Comm:
         with _StdoutToStderr():
             st = load_library().rt_comm_create_all(hs, n, out)
         _check(st)
+        return [cls(c, n, i, b"", _handle=ctypes.c_void_p(out[i])) for i, c in enumerate(ctxs)]
+
+    @classmethod
+    def create_local(cls, ctxs: list) -> list:
+        """n communicators over n contexts of this process that may share a GPU
+        (rt_comm_create_local: the gather as device copies); driven by render_gather_all."""
+        n = len(ctxs)
+        hs = (ctypes.c_void_p * n)(*[c.handle for c in ctxs])
+        out = (ctypes.c_void_p * n)()
+        _check(load_library().rt_comm_create_local(hs, n, out))
         return [cls(c, n, i, b"", _handle=ctypes.c_void_p(out[i])) for i, c in enumerate(ctxs)]
 
     @property

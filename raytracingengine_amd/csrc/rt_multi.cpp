@@ -33,6 +33,11 @@ struct rt_comm {
     rt_context* ctx = nullptr;  // the context whose device and stream the renders use
     int device = -1;
     ncclComm_t nccl = nullptr;
+    // rt_comm_create_local: no RCCL communicator; rt_render_gather_all copies every rank's rows
+    // into rank 0's receive buffer (`peers` = the group in rank order, on every member)
+    bool local = false;
+    std::vector<rt_comm*> peers;
+    hipEvent_t xfer_ready = nullptr, xfer_done = nullptr;
     int nranks = 1, rank = 0;
     // Two frame slots (RT_FLAG_PIPELINE alternates them; otherwise slot 0).  Per slot and output
     // kind (RT_OUT_HDR64, _HDR32, _LDR): this rank's packed rows (send) and, on rank 0, the n
@@ -133,6 +138,7 @@ struct Frame {
     rt_comm::Ev* ev = nullptr;
     int slot = 0;
     bool pipelined = false;
+    bool direct = false;       // one rank: rendered into the framebuffers, nothing to gather
     hipStream_t gs = nullptr;  // the stream of the gather and the assembly
 };
 
@@ -144,18 +150,21 @@ rt_status record(rt_comm::Ev* ev, int k, hipStream_t s) {
 
 // Phase 1 of a frame on one rank: this rank's rows rendered into its send buffers.
 rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
-                      const rt_render_opts* opts, int outputs, Frame& f) {
+                      const rt_render_opts* opts, int outputs, void* const* dst, Frame& f) {
     rt_context* ctx = c->ctx;
     if (sc->ctx != ctx)
         return fail(RT_ERR_INVALID_ARG, "scene does not belong to the communicator's context");
     rt_status st = make_plan(cam, opts, c->nranks, c->rank, f.pl);
     if (st != RT_OK) return st;
     Plan& pl = f.pl;
-    f.pipelined = (pl.opts.flags & RT_FLAG_PIPELINE) != 0;
+    // one rank: its rows are the whole frame in image order, rendered straight into the
+    // caller's framebuffers (no send buffer, no gather, no assembly)
+    f.direct = c->nranks == 1;
+    f.pipelined = !f.direct && (pl.opts.flags & RT_FLAG_PIPELINE) != 0;
     f.slot = f.pipelined ? static_cast<int>(c->frame & 1) : 0;
     f.gs = f.pipelined ? c->gstream : ctx->stream;
     const size_t npx = static_cast<size_t>(pl.max_rows) * cam->width;
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 3 && !f.direct; ++k) {
         if (!(outputs & kOutputs[k])) continue;
         RT_HIP(c->send[f.slot][k].ensure(npx * bytes_per_px(k)));
         if (c->rank == 0) RT_HIP(c->recv[f.slot][k].ensure(npx * bytes_per_px(k) * c->nranks));
@@ -191,11 +200,11 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
     st = record(f.ev, 0, ctx->stream);
     if (st != RT_OK) return st;
     if (pl.rows > 0) {
-        DeviceBuffer* sb = c->send[f.slot];
-        st = enqueue_render(ctx, sc, cam, &pl.opts,
-                            (outputs & RT_OUT_HDR64) ? static_cast<double*>(sb[0].ptr) : nullptr,
-                            (outputs & RT_OUT_HDR32) ? static_cast<float*>(sb[1].ptr) : nullptr,
-                            (outputs & RT_OUT_LDR) ? static_cast<uint8_t*>(sb[2].ptr) : nullptr);
+        void* out[3];
+        for (int k = 0; k < 3; ++k)
+            out[k] = !(outputs & kOutputs[k]) ? nullptr : (f.direct ? dst[k] : c->send[f.slot][k].ptr);
+        st = enqueue_render(ctx, sc, cam, &pl.opts, static_cast<double*>(out[0]),
+                            static_cast<float*>(out[1]), static_cast<uint8_t*>(out[2]));
         if (st != RT_OK) return st;
     }
     st = record(f.ev, 1, ctx->stream);
@@ -209,6 +218,7 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
 
 // Phase 2: one ncclGather per output (inside the caller's group).
 rt_status gather_part(rt_comm* c, const rt_camera* cam, int outputs, const Frame& f) {
+    if (f.direct) return RT_OK;
     const size_t npx = static_cast<size_t>(f.pl.max_rows) * cam->width;
     for (int k = 0; k < 3; ++k) {
         if (!(outputs & kOutputs[k])) continue;
@@ -219,12 +229,55 @@ rt_status gather_part(rt_comm* c, const rt_camera* cam, int outputs, const Frame
     return RT_OK;
 }
 
+// Phase 2 of local communicators (rt_comm_create_local, every rank in this process): rank r's
+// padded send buffer into slot r of rank 0's receive buffer, as ncclGather lays it out.  Rank
+// 0's gather stream waits for every rank's rows; every other rank's gather stream then waits
+// for rank 0's copies, so its send slot is handed back (freed) only once it has been read.
+rt_status gather_local(rt_comm* const* comms, int n, const rt_camera* cam, int outputs,
+                       const std::vector<Frame>& f) {
+    rt_comm* root = comms[0];
+    const Frame& f0 = f[0];
+    if (f0.direct) return RT_OK;
+    const size_t npx = static_cast<size_t>(f0.pl.max_rows) * cam->width;
+    for (int i = 0; i < n; ++i) {
+        rt_comm* c = comms[i];
+        if (f[i].gs != f0.gs) {
+            DeviceGuard g(c->device);
+            RT_HIP(hipEventRecord(c->xfer_ready, f[i].gs));
+            DeviceGuard g0(root->device);
+            RT_HIP(hipStreamWaitEvent(f0.gs, c->xfer_ready, 0));
+        }
+    }
+    DeviceGuard g0(root->device);
+    for (int k = 0; k < 3; ++k) {
+        if (!(outputs & kOutputs[k])) continue;
+        const size_t bytes = npx * bytes_per_px(k);
+        char* recv = static_cast<char*>(root->recv[f0.slot][k].ptr);
+        for (int i = 0; i < n; ++i) {
+            const void* send = comms[i]->send[f[i].slot][k].ptr;
+            if (comms[i]->device == root->device)
+                RT_HIP(hipMemcpyAsync(recv + i * bytes, send, bytes, hipMemcpyDeviceToDevice,
+                                      f0.gs));
+            else
+                RT_HIP(hipMemcpyPeerAsync(recv + i * bytes, root->device, send,
+                                          comms[i]->device, bytes, f0.gs));
+        }
+    }
+    RT_HIP(hipEventRecord(root->xfer_done, f0.gs));
+    for (int i = 1; i < n; ++i) {
+        if (f[i].gs == f0.gs) continue;
+        DeviceGuard g(comms[i]->device);
+        RT_HIP(hipStreamWaitEvent(f[i].gs, root->xfer_done, 0));
+    }
+    return RT_OK;
+}
+
 // Phase 3 (rank 0): gathered rows into image order in the caller's device framebuffers.
 rt_status assemble_part(rt_comm* c, const rt_camera* cam, int outputs, const Frame& f,
                         void* const* dst) {
     rt_status st = record(f.ev, 3, f.gs);
     if (st != RT_OK) return st;
-    if (c->rank == 0) {
+    if (c->rank == 0 && !f.direct) {
         for (int k = 0; k < 3; ++k) {
             if (!(outputs & kOutputs[k]) || !dst[k]) continue;
             RT_HIP(launch_assemble_rows(c->recv[f.slot][k].ptr, dst[k],
@@ -246,6 +299,8 @@ rt_status assemble_part(rt_comm* c, const rt_camera* cam, int outputs, const Fra
 // The gather stream and the slot hand-over events (the caller holds a DeviceGuard).
 rt_status init_streams(rt_comm* c) {
     RT_HIP(hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
+    RT_HIP(hipEventCreateWithFlags(&c->xfer_ready, hipEventDisableTiming));
+    RT_HIP(hipEventCreateWithFlags(&c->xfer_done, hipEventDisableTiming));
     for (int s = 0; s < 2; ++s) {
         RT_HIP(hipEventCreateWithFlags(&c->rendered[s], hipEventDisableTiming));
         RT_HIP(hipEventCreateWithFlags(&c->freed[s], hipEventDisableTiming));
@@ -262,9 +317,9 @@ rt_status check_root_outputs(const rt_comm* c, int outputs, void* const* dst) {
     return RT_OK;
 }
 
-// Contexts that share a GPU (RCCL allows one rank per GPU): the same block-cyclic split, each
-// context's rows copied straight into the caller's host rows (every device's copies are
-// enqueued before the first synchronisation, so the devices' transfers overlap).
+// RTAMD_MULTI_HOST=1: the same block-cyclic split, each context's rows copied straight into the
+// caller's host rows (every device's copies are enqueued before the first synchronisation, so
+// the devices' transfers overlap).
 rt_status render_multi_host(rt_context* const* ctxs, rt_scene* const* scenes, int n,
                             const rt_camera* cam, const rt_render_opts* opts, double* h64,
                             float* h32, uint8_t* hldr, rt_stats* stats) {
@@ -359,18 +414,22 @@ rt_status render_multi_host(rt_context* const* ctxs, rt_scene* const* scenes, in
 // One frame over n contexts into host framebuffers (rt_capi.h rt_render_multi).  Distinct GPUs:
 // the RCCL path — communicators over the contexts' devices (ncclCommInitAll, cached in ctxs[0]
 // until the context list changes), rt_render_gather_all into ctxs[0]'s device framebuffers,
-// one device-to-host copy per output from rank 0.
-rt_status render_multi_rccl(rt_context* const* ctxs, rt_scene* const* scenes, int n,
-                            const rt_camera* cam, const rt_render_opts* opts, int outputs,
-                            double* h64, float* h32, uint8_t* hldr, rt_stats* stats) {
+// one device-to-host copy per output from rank 0.  Contexts sharing a GPU: the same with local
+// communicators (rt_comm_create_local: the gather as device copies).
+rt_status render_multi_group(rt_context* const* ctxs, rt_scene* const* scenes, int n,
+                             const rt_camera* cam, const rt_render_opts* opts, int outputs,
+                             bool local, double* h64, float* h32, uint8_t* hldr,
+                             rt_stats* stats) {
     rt_context* root = ctxs[0];
     bool same = root->group_ctxs.size() == static_cast<size_t>(n);
     for (int i = 0; same && i < n; ++i)
-        same = root->group_ctxs[i] == ctxs[i] && root->group_comms[i]->device == ctxs[i]->device;
+        same = root->group_ctxs[i] == ctxs[i] && root->group_comms[i]->device == ctxs[i]->device &&
+               root->group_comms[i]->local == local;
     if (!same) {
         release_group(root);
         std::vector<rt_comm*> comms(static_cast<size_t>(n), nullptr);
-        rt_status st = rt_comm_create_all(ctxs, n, comms.data());
+        rt_status st = local ? rt_comm_create_local(ctxs, n, comms.data())
+                             : rt_comm_create_all(ctxs, n, comms.data());
         if (st != RT_OK) return st;
         root->group_ctxs.assign(ctxs, ctxs + n);
         root->group_comms = comms;
@@ -462,12 +521,13 @@ rt_status rt_render_multi(rt_context* const* ctxs, rt_scene* const* scenes, int 
     const int outputs = (h64 ? RT_OUT_HDR64 : 0) | (h32 ? RT_OUT_HDR32 : 0) |
                         (hldr ? RT_OUT_LDR : 0);
     const char* env = std::getenv("RTAMD_MULTI_HOST");  // force the host assembly (tests)
-    if (distinct && outputs && !(env && std::atoi(env) == 1)) {
+    if (outputs && !(env && std::atoi(env) == 1)) {
         rt_render_opts o;
         if (opts) o = *opts;
         else rt_render_opts_default(&o);
         if (!hldr) o.tonemap = RT_TONEMAP_NONE;
-        return render_multi_rccl(ctxs, scenes, n, cam, &o, outputs, h64, h32, hldr, stats);
+        return render_multi_group(ctxs, scenes, n, cam, &o, outputs, !distinct, h64, h32, hldr,
+                                  stats);
     }
     return render_multi_host(ctxs, scenes, n, cam, opts, h64, h32, hldr, stats);
 }
@@ -577,6 +637,40 @@ rt_status rt_comm_create_all(rt_context* const* ctxs, int n, rt_comm** out) {
     return RT_OK;
 }
 
+rt_status rt_comm_create_local(rt_context* const* ctxs, int n, rt_comm** out) {
+    if (!ctxs || !out || n < 1) return fail(RT_ERR_INVALID_ARG, "rt_comm_create_local: n < 1 or NULL");
+    for (int i = 0; i < n; ++i) {
+        if (!ctxs[i]) return fail(RT_ERR_INVALID_ARG, "rt_comm_create_local: NULL context");
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i])  // each rank renders into its own buffers on its own stream
+                return fail(RT_ERR_INVALID_ARG, "rt_comm_create_local: context repeated");
+    }
+    std::vector<rt_comm*> peers(static_cast<size_t>(n), nullptr);
+    for (int i = 0; i < n; ++i) {
+        rt_comm* c = new (std::nothrow) rt_comm();
+        rt_status st = c ? RT_OK : fail(RT_ERR_OOM, "host allocation failed");
+        if (c) {
+            c->ctx = ctxs[i];
+            c->device = ctxs[i]->device;
+            c->local = true;
+            c->nranks = n;
+            c->rank = i;
+            peers[static_cast<size_t>(i)] = c;
+            DeviceGuard g(c->device);
+            st = init_streams(c);
+        }
+        if (st != RT_OK) {
+            for (rt_comm* p : peers) rt_comm_destroy(p);
+            return st;
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        peers[static_cast<size_t>(i)]->peers = peers;
+        out[i] = peers[static_cast<size_t>(i)];
+    }
+    return RT_OK;
+}
+
 rt_status rt_comm_destroy(rt_comm* c) {
     if (!c) return RT_OK;
     DeviceGuard g(c->device);
@@ -596,6 +690,8 @@ rt_status rt_comm_destroy(rt_comm* c) {
         if (c->rendered[s]) (void)hipEventDestroy(c->rendered[s]);
         if (c->freed[s]) (void)hipEventDestroy(c->freed[s]);
     }
+    if (c->xfer_ready) (void)hipEventDestroy(c->xfer_ready);
+    if (c->xfer_done) (void)hipEventDestroy(c->xfer_done);
     if (c->gstream) (void)hipStreamDestroy(c->gstream);
     delete c;
     return RT_OK;
@@ -618,14 +714,19 @@ rt_status rt_render_gather(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
     void* const dst[3] = {d_hdr64, d_hdr32, d_ldr};
     if (st == RT_OK) st = check_root_outputs(c, outputs, dst);
     if (st != RT_OK) return st;
+    if (c->local && c->nranks > 1)
+        return fail(RT_ERR_INVALID_ARG, "local communicators (rt_comm_create_local) gather "
+                                        "through rt_render_gather_all");
     DeviceGuard g(c->device);
     Frame f;
-    st = render_part(c, sc, cam, opts, outputs, f);
+    st = render_part(c, sc, cam, opts, outputs, dst, f);
     if (st != RT_OK) return st;
-    RT_NCCL(ncclGroupStart());
-    st = gather_part(c, cam, outputs, f);
-    RT_NCCL(ncclGroupEnd());
-    if (st != RT_OK) return st;
+    if (!f.direct) {
+        RT_NCCL(ncclGroupStart());
+        st = gather_part(c, cam, outputs, f);
+        RT_NCCL(ncclGroupEnd());
+        if (st != RT_OK) return st;
+    }
     return assemble_part(c, cam, outputs, f, dst);
 }
 
@@ -637,25 +738,33 @@ rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, i
     if (st == RT_OK) st = check_outputs(outputs);
     if (st != RT_OK) return st;
     for (int i = 0; i < n; ++i)
-        if (!comms[i] || !scenes[i] || comms[i]->nranks != n || comms[i]->rank != i)
+        if (!comms[i] || !scenes[i] || comms[i]->nranks != n || comms[i]->rank != i ||
+            comms[i]->local != comms[0]->local ||
+            (comms[0]->local && comms[0]->peers[static_cast<size_t>(i)] != comms[i]))
             return fail(RT_ERR_INVALID_ARG, "rt_render_gather_all: comms must be the n ranks of "
-                                            "one rt_comm_create_all, in rank order");
+                                            "one rt_comm_create_all / rt_comm_create_local, in "
+                                            "rank order");
     void* const dst[3] = {d_hdr64, d_hdr32, d_ldr};
     st = check_root_outputs(comms[0], outputs, dst);
     if (st != RT_OK) return st;
     std::vector<Frame> f(static_cast<size_t>(n));
     for (int i = 0; i < n; ++i) {  // 1. every GPU renders its rows (asynchronous)
         DeviceGuard g(comms[i]->device);
-        st = render_part(comms[i], scenes[i], cam, opts, outputs, f[i]);
+        st = render_part(comms[i], scenes[i], cam, opts, outputs, dst, f[i]);
         if (st != RT_OK) return st;
     }
-    RT_NCCL(ncclGroupStart());  // 2. one gather per output over all GPUs
-    for (int i = 0; i < n && st == RT_OK; ++i) {
-        DeviceGuard g(comms[i]->device);
-        st = gather_part(comms[i], cam, outputs, f[i]);
+    if (comms[0]->local) {  // 2. the gather as device copies into rank 0's receive buffer
+        st = gather_local(comms, n, cam, outputs, f);
+        if (st != RT_OK) return st;
+    } else if (!f[0].direct) {  // 2. one gather per output over all GPUs
+        RT_NCCL(ncclGroupStart());
+        for (int i = 0; i < n && st == RT_OK; ++i) {
+            DeviceGuard g(comms[i]->device);
+            st = gather_part(comms[i], cam, outputs, f[i]);
+        }
+        RT_NCCL(ncclGroupEnd());
+        if (st != RT_OK) return st;
     }
-    RT_NCCL(ncclGroupEnd());
-    if (st != RT_OK) return st;
     for (int i = 0; i < n; ++i) {  // 3. rank 0 assembles; the others close their events
         DeviceGuard g(comms[i]->device);
         st = assemble_part(comms[i], cam, outputs, f[i], dst);

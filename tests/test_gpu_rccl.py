@@ -1,10 +1,14 @@
 """The RCCL multi-GPU frame path behind the C-ABI (rt_multi.cpp; SURVEY.md §8e, RE/Scene.h:318-325).
 
-The test box has ONE MI355X and RCCL allows one rank per GPU, so the collective itself runs here
-with n = 1 (rank 0 gathers from itself over the same code path: render into the send buffer,
-ncclGather, assembly into image order); the row plans of n > 1 ranks are pinned through the
-assembly hook (rt_debug_assemble_rows) against the Python row planner, and the multi-rank
-gather end-to-end runs on CPU with gloo (tests/test_distributed_cpu.py).
+The test box has ONE MI355X and RCCL allows one rank per GPU ("Duplicate GPU detected"), so
+ncclGather itself only runs here with n = 1 (where the rank now renders straight into the frame).
+The n > 1 frame runs end to end on the one GPU through LOCAL communicators
+(rt_comm_create_local): n contexts, each on its own stream, render their block-cyclic rows into
+padded send buffers; the gather is a device copy of every rank's buffer into rank 0's receive
+buffer at rank r's offset (what ncclGather delivers); rank 0 assembles — every line of
+rt_multi.cpp's multi-rank frame except the ncclGather call.  The row plans are also pinned through
+the assembly hook (rt_debug_assemble_rows) against the Python row planner, and the multi-rank
+gather of the Python driver runs on CPU with gloo (tests/test_distributed_cpu.py).
 """
 import hashlib
 
@@ -55,7 +59,8 @@ def test_render_gather_one_rank_equals_render(ctx, comm1, name, w, h):
         ds.close()
     t = comm1.timing(reset=True)
     assert t.frames == 2 and t.rows == h and t.max_rows == h
-    assert t.render_ms > 0 and t.gather_ms >= 0 and t.assemble_ms > 0
+    # one rank renders straight into the framebuffers: nothing to gather or assemble
+    assert t.render_ms > 0 and t.gather_ms >= 0 and t.assemble_ms >= 0
 
 
 def test_render_gather_ldr_only_full_c4(ctx, comm1, golden):
@@ -179,4 +184,133 @@ def test_render_gather_pipelined_frames(ctx, comm1):
     finally:
         ds.close()
     t = comm1.timing(reset=True)
-    assert t.frames == 5 and t.render_ms > 0 and t.assemble_ms > 0
+    assert t.frames == 5 and t.render_ms > 0 and t.assemble_ms >= 0
+
+
+@pytest.fixture(scope="module")
+def local_ctxs():
+    cs = [capi.Context(0) for _ in range(8)]
+    yield cs
+    for c in cs:
+        c.close()
+
+
+def _local_frame(ctxs, sc, n, outputs, flags=0, row_block=0, frames=1, cams=None):
+    """n local ranks render `frames` frames of `sc` (one camera per frame) through
+    rt_render_gather_all; returns the host copies of rank 0's framebuffers per frame."""
+    W, H = sc.camera.width, sc.camera.height
+    comms = capi.Comm.create_local(ctxs[:n])
+    scenes = [c.scene(sc) for c in ctxs[:n]]
+    try:
+        outs = []
+        for k in range(frames):
+            if cams is not None:
+                for ds in scenes:
+                    ds.camera["position"][0] = cams[k]
+            bufs = {"hdr64": torch.zeros(H * W * 3, dtype=torch.float64, device="cuda"),
+                    "hdr32": torch.zeros(H * W * 3, dtype=torch.float32, device="cuda"),
+                    "ldr": torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda")}
+            ptr = {k2: (v.data_ptr() if outputs & bit else None) for (k2, v), bit in
+                   zip(bufs.items(), (capi.RT_OUT_HDR64, capi.RT_OUT_HDR32, capi.RT_OUT_LDR))}
+            capi.render_gather_all(comms, scenes,
+                                   capi.default_opts(tonemap=1, flags=flags, row_block=row_block),
+                                   outputs, ptr["hdr64"], ptr["hdr32"], ptr["ldr"])
+            outs.append(bufs)
+        for c in comms:
+            c.synchronize()
+        timing = [c.timing(reset=True) for c in comms]
+        host = [{k2: v.cpu().numpy().reshape(H, W, 3) for k2, v in b.items()} for b in outs]
+        return host, timing
+    finally:
+        for c in comms:
+            c.close()
+        for ds in scenes:
+            ds.close()
+
+
+@pytest.mark.parametrize("name,w,h,n,block", [
+    ("c2", 640, 360, 2, 0), ("c2", 640, 360, 8, 0), ("c3", 640, 360, 3, 7),
+    ("c5", 320, 180, 4, 16), ("glass", 200, 120, 2, 5), ("mirror", 320, 180, 5, 0),
+    ("c2", 96, 40, 8, 16)])  # the last: ranks 3..7 have no rows (padding only)
+def test_local_ranks_frame_equals_render(ctx, local_ctxs, name, w, h, n, block):
+    """n > 1 ranks of the multi-rank frame on one GPU (local communicators): every output equals
+    rt_render, with the row plan's padding, empty ranks and per-rank timings."""
+    sc = make_config(name, w, h)
+    ds = ctx.scene(sc)
+    try:
+        ref = ds.render(hdr64=True, hdr32=True, tonemap=1)
+    finally:
+        ds.close()
+    outs = capi.RT_OUT_HDR64 | capi.RT_OUT_HDR32 | capi.RT_OUT_LDR
+    host, timing = _local_frame(local_ctxs, sc, n, outs, flags=capi.RT_FLAG_TIME_KERNEL,
+                                row_block=block)
+    assert np.array_equal(host[0]["hdr64"], ref["hdr64"])
+    assert np.array_equal(host[0]["hdr32"], ref["hdr32"])
+    assert np.array_equal(host[0]["ldr"], ref["ldr"])
+    b = block or 16
+    plans = [[(a, min(c, h)) for a, c in row_ranges(r, n, h, b) if a < h] for r in range(n)]
+    rows = [plan_rows(p) for p in plans]
+    assert [t.rows for t in timing] == rows
+    assert all(t.max_rows == max(rows) and t.frames == 1 for t in timing)
+    assert timing[0].assemble_ms > 0
+
+
+def test_local_ranks_pipelined_frames(local_ctxs):
+    """RT_FLAG_PIPELINE with 4 local ranks: five frames from five cameras enqueued back to back
+    (frame k's gather + assembly overlap frame k+1's render, two send/receive slots per rank),
+    each equal to rt_render of its camera."""
+    sc = make_config("c3", 640, 360)
+    base = np.array(sc.camera.position)
+    cams = [base + (0.5 * k, -0.25 * k, 0.0) for k in range(5)]
+    refs = []
+    ds = local_ctxs[7].scene(sc)
+    try:
+        for cpos in cams:
+            ds.camera["position"][0] = cpos
+            refs.append(ds.render(hdr64=False, tonemap=1)["ldr"])
+    finally:
+        ds.close()
+    host, timing = _local_frame(local_ctxs, sc, 4, capi.RT_OUT_LDR,
+                                flags=capi.RT_FLAG_PIPELINE | capi.RT_FLAG_TIME_KERNEL,
+                                frames=5, cams=cams)
+    for k in range(5):
+        assert np.array_equal(host[k]["ldr"], refs[k]), k
+    assert all(t.frames == 5 for t in timing)
+
+
+def test_local_8_ranks_full_c4_reference_bytes(local_ctxs, golden):
+    """The bench's N=8 workload on one GPU: the full 7680x4320 C4 frame split over 8 ranks in
+    16-row blocks, gathered into rank 0 and assembled — the reference's Reinhard bytes."""
+    sc = make_config("c4")
+    host, timing = _local_frame(local_ctxs, sc, 8, capi.RT_OUT_LDR)
+    assert _sha(host[0]["ldr"]) == golden["meta"]["scenes"]["c4_full"]["ldr_sha256"][
+        "reinhard_simple"]
+    assert sum(t.rows for t in timing) == sc.camera.height
+
+
+def test_render_multi_shared_device_group_lifetime():
+    """rt_render_multi over contexts that share the GPU goes through local communicators cached
+    in the first context.  Destroying a NON-root member first releases that cached group (no
+    communicator is left pointing at the dead context); a new context list rebuilds it."""
+    sc = make_config("c2", 320, 180)
+    cs = [capi.Context(0) for _ in range(3)]
+    try:
+        ref_ds = cs[0].scene(sc)
+        ref = ref_ds.render(hdr64=True, tonemap=1, stats=True)
+        scenes = [c.scene(sc) for c in cs]
+        for _ in range(2):  # the second call reuses the cached group
+            m = capi.render_multi(scenes, hdr64=True, tonemap=1, stats=True)
+            assert np.array_equal(m["hdr64"], ref["hdr64"])
+            assert np.array_equal(m["ldr"], ref["ldr"])
+            assert (m["trace_rays"], m["shadow_rays"]) == (ref["trace_rays"], ref["shadow_rays"])
+        scenes[1].close()
+        cs[1].close()                       # a member of cs[0]'s group goes first
+        cs[1] = capi.Context(0)
+        scenes[1] = cs[1].scene(sc)
+        m = capi.render_multi([scenes[0], scenes[2], scenes[1]], hdr64=True, tonemap=1)
+        assert np.array_equal(m["hdr64"], ref["hdr64"])
+        for ds in scenes + [ref_ds]:
+            ds.close()
+    finally:
+        for c in cs:
+            c.close()                       # root first this time, then the members

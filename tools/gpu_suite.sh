@@ -1,14 +1,16 @@
 #!/bin/bash
-# GPU call (dev tool): the GPU test suite, smoke(), and the default bench line of the current
-# tree, each under its own time limit.   bash tools/gpu_suite.sh TAG
+# GPU call (dev tool): the GPU test suite (with -s: the parity tests print their byte-flip
+# counts, "FLIPS ..."), smoke(), and the default bench line of the current tree, each under its
+# own time limit.   bash tools/gpu_suite.sh TAG
 set -u
 TAG=${1:-suite}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -s --timeout 200 --timeout-method thread \
     -p no:cacheprovider > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
 tail -1 $OUT/gpu_tests.log
+grep FLIPS $OUT/gpu_tests.log > $OUT/flips.txt || true
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
     > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
