@@ -150,6 +150,7 @@ __device__ __forceinline__ SceneView global_view(const TraceParams& P) {
     S.np = P.np;
     S.nt = P.nt;
     S.nl = P.nl;
+    S.pl_axis = P.pl_axis;
     S.sph = P.sph;
     S.pl = P.pl;
     S.lt = P.lt;
