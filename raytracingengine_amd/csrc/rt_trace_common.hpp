@@ -50,12 +50,10 @@ __device__ __forceinline__ bool axis_ray_ok(d3 o, d3 d) {
     return fabs(o.x) + fabs(o.y) + fabs(o.z) <= kAxisOrigin &&
            fabs(d.x) + fabs(d.y) + fabs(d.z) <= kAxisDir;
 }
-// f(o_k, d_k, k) for a wave-uniform axis k: a scalar branch, no per-lane select
-template <class F>
-__device__ __forceinline__ void on_axis(int k, d3 o, d3 d, F&& f) {
-    if (k == 0) f(o.x, d.x, 0);
-    else if (k == 1) f(o.y, d.y, 1);
-    else f(o.z, d.z, 2);
+// Component k (wave-uniform) of v: selects on a scalar condition (scalar branches into three
+// copies of the plane code cost the packet kernel 36 B/lane of spills)
+__device__ __forceinline__ double axis_comp(d3 v, int k) {
+    return k == 0 ? v.x : (k == 1 ? v.y : v.z);
 }
 // Plane::Intersect through the axis shortcut for a closest-hit search that holds `best`:
 // 0 = no hit that could replace it, 1 = hit at t (t >= 0, not provably >= best), 2 = c == 0,
@@ -241,17 +239,16 @@ __device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) 
         const int ax = plane_axis(S.pl_axis, i);  // uniform
         bool literal = true;
         if (ax != 0 && axis_ok) {
-            on_axis(ax - 1, o, d, [&](double ok, double dk, int k) {
-                double t;
-                const int r = axis_plane_t(p[k], ok, dk, found, best, t);
-                literal = r == 2;
-                if (r == 1 && (!found || t < best)) {
-                    found = true;
-                    best = t;
-                    kind = 2;
-                    idx = i;
-                }
-            });
+            const int k = ax - 1;
+            double t;
+            const int r = axis_plane_t(p[k], axis_comp(o, k), axis_comp(d, k), found, best, t);
+            literal = r == 2;
+            if (r == 1 && (!found || t < best)) {
+                found = true;
+                best = t;
+                kind = 2;
+                idx = i;
+            }
         }
         if (!literal) continue;
         const d3 n = mk(p[3], p[4], p[5]);
@@ -469,12 +466,12 @@ __device__ __forceinline__ int occlusion_opaque(const SceneView& S, d3 o, d3 d, 
         if (ax != 0 && axis_ok) {
             // A = sign(denom)·num = (d_k > 0 ? c : −c), B = |d_k| (c == 0: A = ±0, undecided
             // either way, as the literal code decides it)
-            on_axis(ax - 1, o, d, [&](double ok, double dk, int k) {
-                if (!(fabs(dk) > 1e-6)) return;
-                const double c = p[k] - ok;
-                plane_occlusion_class(dk > 0.0 ? c : -c, fabs(dk), max_dist, bias, blocked,
-                                      undecided);
-            });
+            const int k = ax - 1;
+            const double dk = axis_comp(d, k);
+            if (!(fabs(dk) > 1e-6)) continue;
+            const double c = p[k] - axis_comp(o, k);
+            plane_occlusion_class(dk > 0.0 ? c : -c, fabs(dk), max_dist, bias, blocked,
+                                  undecided);
             continue;
         }
         const d3 n = mk(p[3], p[4], p[5]);

@@ -745,3 +745,92 @@ def test_render_multi_equals_single(name, n, block):
     assert np.array_equal(multi["ldr"], single["ldr"])
     assert (multi["trace_rays"], multi["shadow_rays"]) == (single["trace_rays"],
                                                             single["shadow_rays"])
+
+
+# ------------------------------------------------------------------ axis-aligned planes
+@pytest.mark.parametrize("name,w,h", [("c1", 1000, 1000), ("c2", 1920, 1080), ("c3", 960, 540),
+                                      ("mirror", 640, 360), ("glass", 640, 360),
+                                      ("mesh", 640, 360)])
+def test_axis_planes_equal_literal_dot_products(ctx, name, w, h):
+    """Axis-aligned planes take the exact shortcut t = (p_k − o_k)/d_k (rt_trace_common.hpp:
+    packet, chain and breadth-first kernels); RT_FLAG_NO_AXIS_PLANES renders the same frame
+    through the reference's literal dot products — bit-identical HDR, same ray counts."""
+    sc = make_config(name, w, h)
+    ds = ctx.scene(sc)
+    try:
+        fast = ds.render(hdr64=True, stats=True)
+        lit = ds.render(hdr64=True, stats=True, flags=capi.RT_FLAG_NO_AXIS_PLANES)
+    finally:
+        ds.close()
+    assert np.array_equal(fast["hdr64"], lit["hdr64"])
+    assert (fast["trace_rays"], fast["shadow_rays"]) == (lit["trace_rays"], lit["shadow_rays"])
+
+
+def _axis_box_scene():
+    """Axis-aligned planes with signed-zero normal components, one general plane and one axis
+    plane whose point is beyond the shortcut's 2^1000 bound (literal path)."""
+    sc = _scene(64, 48)
+    sc.add_plane((0, -3, 0), (0.0, 1.0, 0.0), Material((0.8, 0.8, 0.8)))
+    sc.add_plane((0, 0, 10), (-0.0, -0.0, -1.0), Material((0.7, 0.8, 0.9)))
+    sc.add_plane((4, 0, 0), (-1.0, 0.0, -0.0), Material((0.9, 0.3, 0.3)))
+    sc.add_plane((0, 0, 0), (0.0, 0.0, 1.0), Material((0.2, 0.9, 0.2)))       # through o = 0
+    sc.add_plane((3e303, 5.0, 0), (0.0, -1.0, 0.0), Material((0.5, 0.5, 0.5)))  # bound: literal
+    sc.add_plane((0, 6, 0), (0.3, -1.0, 0.2), Material((0.4, 0.4, 0.8)))      # general
+    sc.add_sphere((1, 0, 4), 1.5, Material((0.9, 0.4, 0.2)))
+    sc.add_light((0, 2.5, -2), (1, 1, 1), 40)
+    return sc
+
+
+def test_edge_axis_planes_batch_rays_vs_oracle(ctx, oracle):
+    """IntersectClosest (rt_intersect_rays, the generic closest()) on crafted rays against axis
+    planes: origins exactly on a plane (c == 0: the literal path, ±0 t), directions parallel to
+    a plane or with ±0 components, huge / non-finite origins and directions (outside the
+    shortcut's bounds: literal), against the oracle's literal arithmetic."""
+    sc = _axis_box_scene()
+    rng = np.random.default_rng(11)
+    n = 2048
+    o = rng.uniform(-2.5, 3.5, (n, 3))
+    d = rng.normal(0, 1, (n, 3))
+    o[:64, 1] = -3.0                        # on the floor (c == 0 for the floor)
+    o[64:128, 2] = 0.0                      # on the z = 0 plane, both signs of zero
+    o[96:128, 2] = -0.0
+    o[128:192, 0] = 4.0                     # on the right wall
+    d[192:256, 1] = 0.0                     # parallel to the floor / ceiling
+    d[256:320, 2] = -0.0
+    d[320:336, 0] = 1e-7                    # |d_k| ≤ 1e-6 after normalisation below
+    d[336:352] = [np.inf, 0.3, 0.1]          # non-finite directions
+    d[352:368] = [np.nan, 0.3, 0.1]
+    o[368:384] = [2.0 ** 1021, 0.0, 0.0]     # origin beyond the shortcut's bound
+    d[384:400] *= 2.0 ** 101                 # direction beyond the bound
+    o[400:416] = [np.inf, 0.0, 1.0]
+    with np.errstate(invalid="ignore"):
+        nrm = np.linalg.norm(d[:336], axis=1, keepdims=True)
+        d[:336] = d[:336] / nrm
+    d[320:336, 0] = 1e-7
+    rays = np.concatenate([o, d], axis=1)
+    ds = ctx.scene(sc)
+    try:
+        got = ds.intersect_rays(rays)
+    finally:
+        ds.close()
+    for i, ray in enumerate(rays):
+        typ, idx, vals = oracle.closest(sc, ray)
+        assert int(got[i, 0]) == typ, i
+        if typ:
+            assert int(got[i, 1]) == idx, i
+            assert np.array_equal(got[i, 2:], vals, equal_nan=True), (i, got[i, 2:], vals)
+            # the sign of a zero distance is the reference's too (NaN signs are not IEEE
+            # values: x86 and gfx950 produce differently signed default NaNs)
+            if got[i, 2] == 0.0:
+                assert np.signbit(got[i, 2]) == np.signbit(vals[0]), i
+
+
+@pytest.mark.parametrize("flags", [0, capi.RT_FLAG_GENERIC_KERNEL])
+def test_edge_axis_planes_scene_vs_oracle(ctx, oracle, flags):
+    """The axis box rendered whole (packet kernel and the generic kernel): camera on the z = 0
+    plane's side, shadow rays starting on the walls — bit-identical to the oracle."""
+    sc = _axis_box_scene()
+    out = _render(ctx, sc, hdr64=True, stats=True, flags=flags)
+    ref, nt, ns = oracle.render(sc)
+    assert np.array_equal(out["hdr64"], ref)
+    assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)

@@ -49,6 +49,7 @@ def test_render_gather_one_rank_equals_render(ctx, comm1, name, w, h):
         for k in range(2):
             for t in (d64, d32, d8):
                 t.zero_()
+            torch.cuda.synchronize()  # the fills run on torch's stream, the render on ctx's
             comm1.render_gather(ds, capi.default_opts(tonemap=1, flags=capi.RT_FLAG_TIME_KERNEL),
                                 outs, d64.data_ptr(), d32.data_ptr(), d8.data_ptr())
             ctx.synchronize()
@@ -168,12 +169,14 @@ def test_render_gather_pipelined_frames(ctx, comm1):
             ds.camera["position"][0] = cpos
             refs.append(ds.render(hdr64=False, tonemap=1)["ldr"])
         outs = [torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda") for _ in cams]
+        torch.cuda.synchronize()  # the fills run on torch's stream, the renders on ctx's
         flags = capi.RT_FLAG_PIPELINE | capi.RT_FLAG_TIME_KERNEL
         for cpos, o in zip(cams, outs):
             ds.camera["position"][0] = cpos
             comm1.render_gather(ds, capi.default_opts(tonemap=1, flags=flags), capi.RT_OUT_LDR,
                                 None, None, o.data_ptr())
         serial = torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
         comm1.render_gather(ds, capi.default_opts(tonemap=1), capi.RT_OUT_LDR, None, None,
                             serial.data_ptr())
         comm1.synchronize()
@@ -212,6 +215,7 @@ def _local_frame(ctxs, sc, n, outputs, flags=0, row_block=0, frames=1, cams=None
                     "ldr": torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda")}
             ptr = {k2: (v.data_ptr() if outputs & bit else None) for (k2, v), bit in
                    zip(bufs.items(), (capi.RT_OUT_HDR64, capi.RT_OUT_HDR32, capi.RT_OUT_LDR))}
+            torch.cuda.synchronize()  # the zero fills run on torch's stream, the ranks on theirs
             capi.render_gather_all(comms, scenes,
                                    capi.default_opts(tonemap=1, flags=flags, row_block=row_block),
                                    outputs, ptr["hdr64"], ptr["hdr32"], ptr["ldr"])

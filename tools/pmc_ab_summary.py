@@ -16,5 +16,5 @@ for d in sorted(glob.glob(os.path.join(out, "*"))):
         m = {n: sum(v) / len(v) for n, v in c.items()}
         w = m.get("SQ_WAVES", 1.0)
         print(f"{os.path.basename(d):24s} {k[:48]:48s} waves {w:9.0f} valu/wave {m.get('SQ_INSTS_VALU', 0)/w:7.1f} "
-              f"salu/wave {m.get('SQ_INSTS_SALU', 0)/w:6.1f} trans/wave {m.get('SQ_INSTS_VALU_TRANS_F64', 0)/w:5.1f} "
+              f"salu/wave {m.get('SQ_INSTS_SALU', 0)/w:6.1f} br/wave {m.get('SQ_INSTS_BRANCH', 0)/w:6.1f} lds/wave {m.get('SQ_INSTS_LDS', 0)/w:5.1f} trans/wave {m.get('SQ_INSTS_VALU_TRANS_F64', 0)/w:5.1f} "
               f"active_valu/wave {m.get('SQ_ACTIVE_INST_VALU', 0)/w:7.1f} wave_cycles/wave {m.get('SQ_WAVE_CYCLES', 0)/w:8.1f}")
