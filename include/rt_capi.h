@@ -162,8 +162,6 @@ typedef struct rt_render_opts {
 #define RT_FLAG_TIME_KERNEL 0x2  /* bracket each render launch with HIP events              */
 #define RT_FLAG_GENERIC_KERNEL 0x4 /* ablation: bypass the packet-culled kernel              */
 #define RT_FLAG_NO_BVH 0x8         /* ablation: test every triangle (no triangle BVH)          */
-#define RT_FLAG_NO_AXIS_PLANES 0x20 /* ablation: axis-aligned planes through the literal dot
-                                      products (same bits, slower)                           */
 #define RT_FLAG_PIPELINE 0x10      /* rt_render_gather: gather + assembly on the communicator's
                                       own stream, overlapping the next frame's render (two
                                       frame slots); rt_comm_synchronize waits for the frame   */

@@ -30,7 +30,6 @@ RT_FLAG_TIME_KERNEL = 0x2
 RT_FLAG_GENERIC_KERNEL = 0x4
 RT_FLAG_NO_BVH = 0x8
 RT_FLAG_PIPELINE = 0x10
-RT_FLAG_NO_AXIS_PLANES = 0x20
 RT_OUT_HDR64, RT_OUT_HDR32, RT_OUT_LDR = 0x1, 0x2, 0x4
 RT_COMM_ID_BYTES = 128
 

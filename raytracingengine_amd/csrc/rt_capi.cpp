@@ -58,27 +58,6 @@ uint32_t rendered_rows(const rt_render_opts& o, uint32_t height) {
     return static_cast<uint32_t>(rows);
 }
 
-// Axis code of a plane for the kernels' exact fast path (plane_axis, rt_trace_common.hpp):
-// k + 1 when the normal as stored is exactly ±e_k (two components ±0, the third ±1) and every
-// coordinate of its point is within 2^1000, else 0 (the reference's literal dot products).
-int plane_axis_code(const rt_plane& pl) {
-    int axis = -1, zeros = 0;
-    for (int k = 0; k < 3; ++k) {
-        if (!(std::fabs(pl.point[k]) <= 0x1p1000)) return 0;
-        if (pl.normal[k] == 0.0) ++zeros;
-        else if (pl.normal[k] == 1.0 || pl.normal[k] == -1.0) axis = k;
-    }
-    return zeros == 2 && axis >= 0 ? axis + 1 : 0;
-}
-
-// Camera rays are eligible for the axis-aligned plane path when every camera value is finite
-// and bounded: their directions are then finite (unit vectors or zero) and the origin bounded.
-bool camera_axis_ok(const rt_camera* cam) {
-    for (int k = 0; k < 3; ++k)
-        if (!(std::fabs(cam->position[k]) <= 0x1p1000)) return false;
-    return std::fabs(cam->focal) <= 0x1p1000;
-}
-
 void pack_material(const rt_material& m, double* o) {
     o[0] = m.color[0];
     o[1] = m.color[1];
@@ -206,8 +185,6 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
     }
     p.rows = rows;
     p.tonemap = opts.tonemap;
-    p.pl_axis = sc->pl_axis | (camera_axis_ok(cam) ? kAxisCamOk : 0u);
-    if (opts.flags & RT_FLAG_NO_AXIS_PLANES) p.pl_axis = 0;
 
     // Which TraceRay shape can this scene produce?  (Scene.h:175-195)
     if (sc->any_transparent) path = kPathTree;
@@ -564,7 +541,6 @@ rt_status rt_scene_create(rt_context* ctx, const rt_scene_desc* d, rt_scene** ou
             o[k] = pl.point[k];
             o[3 + k] = pl.normal[k];
         }
-        if (i < kAxisPlanes) sc->pl_axis |= static_cast<uint32_t>(plane_axis_code(pl)) << (2 * i);
         pack_material(pl.material, &h[sc->off_pl_mat + size_t(kMatStride) * i]);
         note(pl.material);
     }

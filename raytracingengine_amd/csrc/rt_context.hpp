@@ -85,7 +85,6 @@ struct rt_scene {
     int32_t ns = 0, np = 0, nt = 0, nl = 0;
     size_t off_sph = 0, off_sph_mat = 0, off_pl = 0, off_pl_mat = 0, off_tri = 0, off_tri_mat = 0,
            off_lt = 0;
-    uint32_t pl_axis = 0;  // axis codes of the planes (TraceParams::pl_axis, camera bit clear)
     bool any_transparent = false;
     double max_specular = 0.0;  // NaN-aware: stored as +inf when a NaN specular exists
     bool has_area = false;

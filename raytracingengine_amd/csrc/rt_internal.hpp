@@ -21,8 +21,6 @@ constexpr int kMatStride = 8;   // r g b shininess specular transparency ior -
 constexpr int kBvhNodeStride = 8;  // triangle BVH node: lo xyz, hi xyz, {first, count}
 constexpr int kBvhMinTris = 32;    // scenes with fewer triangles test them all (no BVH)
 constexpr int kBvhStack = 64;      // traversal stack entries (build depth <= 48)
-constexpr int kAxisPlanes = 15;     // planes whose axis code fits TraceParams::pl_axis
-constexpr uint32_t kAxisCamOk = 1u << 31;
 constexpr int kMaxDepth = 16;   // deepest recursion the CHAIN/TREE kernels keep a stack for
 // Generic kernels: 256-thread workgroups of 8×32 pixels, so each wave is an 8×8 tile — the
 // rays of a square tile stay together down a reflection chain longer than those of a 64-pixel
@@ -69,10 +67,7 @@ struct TraceParams {
     float* out32;
     uint8_t* ldr;
     int32_t tonemap;
-    // Axis-aligned planes (rt_scene_create): 2 bits per plane i < kAxisPlanes, 0 = general,
-    // k + 1 = the stored normal is exactly ±e_k (plane_axis, rt_trace_common.hpp); bit 31 =
-    // the camera is finite and bounded, so every camera ray is eligible for the fast path.
-    uint32_t pl_axis;
+    int32_t _pad;
     unsigned long long* counters;  // [trace, shadow] — only written by the counting variant
     const uint8_t* redo;  // generic kernels: when set, only pixels with a flagged sample run
     const double* bvh;       // triangle BVH nodes (rt_bvh.cpp), or null: test every triangle
@@ -86,6 +81,8 @@ struct TraceParams {
     // packet kernel, ns >= kSphChunkMin: spatial sphere order and chunk bounds (build_sphere_chunks)
     const int32_t* sph_perm;
     const double* sph_bnd;
+    // generic kernels with `redo`: 0 here means no sample overflowed, every workgroup leaves
+    const uint32_t* redo_any;
 };
 
 // Host: the spatial sphere chunks of the packet kernel's culls (rt_bvh.cpp): perm[sorted] =

@@ -55,17 +55,6 @@ constexpr double kNoWin = 1.0 + 0x1.0p-40;  // "quotient provably >= best" facto
 #define RT_SHADOW_SPLIT_MIN 16
 #endif
 constexpr bool kShadowSplit = RT_SHADOW_SPLIT != 0;
-// Axis-aligned plane shortcut (rt_trace_common.hpp) per use: camera rays, shadow-ray
-// classification, the exact march.
-#ifndef RT_AXIS_CAM
-#define RT_AXIS_CAM 1
-#endif
-#ifndef RT_AXIS_OCC
-#define RT_AXIS_OCC 1
-#endif
-#ifndef RT_AXIS_MARCH
-#define RT_AXIS_MARCH 0  // the march is the rare undecided path: +8 B/lane of spills on C2
-#endif
 constexpr int kShadowSplitMin = RT_SHADOW_SPLIT_MIN;
 
 // Feature bits of a kernel variant: code for a feature the scene does not use is not compiled
@@ -147,7 +136,6 @@ struct PacketScene {
     // and orig[i] is sorted sphere i's index in the scene (material table, closest-hit ties)
     const int32_t* orig;
     int ns, np, nt, nl, nb;
-    uint32_t pl_axis;  // axis-aligned plane codes (TraceParams::pl_axis, rt_trace_common.hpp)
 };
 
 // Closest hit of the packet kernel: t and the primitive's index in the material table order
@@ -513,15 +501,9 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
             }
         }
     }
-    const bool cam_axis = RT_AXIS_CAM && (S.pl_axis & kAxisCamOk) != 0;  // finite, bounded rays
     for (int i = 0; i < S.np; ++i) {
         const double* p = S.pl + kPlStride * i;
-        const int ax = cam_axis ? plane_axis(S.pl_axis, i) : 0;  // uniform
-        double denom;
-        if (ax != 0)  // n = ±e_k: n·d = n_k·d_k whenever it is nonzero (rt_trace_common.hpp)
-            denom = p[3 + ax - 1] * axis_comp(d, ax - 1);
-        else
-            denom = dot(mk(p[3], p[4], p[5]), d);
+        const double denom = dot(mk(p[3], p[4], p[5]), d);
         if (p[7] != 0.0) plane_t_core(p[6], denom, S.ns + i, found, best, prim);  // uniform
         else plane_t(p[6], denom, S.ns + i, found, best, prim);
     }
@@ -557,23 +539,8 @@ __device__ __forceinline__ bool closest_masked(const PacketScene& S, const Masks
             else sphere_roots_literal<(MAXC > 1)>(b, disc, two_a, i, S.orig, found, best, prim);
         }
     }
-    const bool axis_ok = RT_AXIS_MARCH && S.pl_axis != 0 && axis_ray_ok(o, d);
     for (int i = 0; i < S.np; ++i) {
         const double* p = S.pl + kPlStride * i;
-        const int ax = RT_AXIS_MARCH ? plane_axis(S.pl_axis, i) : 0;  // uniform
-        bool literal = true;
-        if (ax != 0 && axis_ok) {
-            const int k = ax - 1;
-            double t;
-            const int r = axis_plane_t(p[k], axis_comp(o, k), axis_comp(d, k), found, best, t);
-            literal = r == 2;
-            if (r == 1 && (!found || t < best)) {
-                found = true;
-                best = t;
-                prim = S.ns + i;
-            }
-        }
-        if (!literal) continue;
         const d3 n = mk(p[3], p[4], p[5]);
         plane_t(dot(mk(p[0], p[1], p[2]) - o, n), dot(n, d), S.ns + i, found, best, prim);
     }
@@ -692,29 +659,21 @@ __device__ __forceinline__ int pk_occlusion(const PacketScene& S, const Masks<MA
             else undecided = true;                            // near hit or on a boundary
         }
     }
-    const bool axis_ok = RT_AXIS_OCC && S.pl_axis != 0 && axis_ray_ok(o, d);
     for (int i = 0; i < S.np; ++i) {
         if (i < 64 && ((M.pm >> i) & 1ull) == 0) continue;  // clear for the whole packet (uniform)
         // Plane::Intersect (Shape.h:149-159): t = num / denom, decided without the division:
         // with A = num·sign(denom), B = |denom|, t lies on the side of x that A lies of x·B
-        // (plane_occlusion_class, rt_trace_common.hpp)
+        // (1e-9 relative margin ≫ the FP64 rounding of the quotient and the product)
         const double* p = S.pl + kPlStride * i;
-        const int ax = RT_AXIS_OCC ? plane_axis(S.pl_axis, i) : 0;  // uniform
-        if (ax != 0 && axis_ok) {  // n = ±e_k: A = (d_k > 0 ? c : −c), B = |d_k|
-            const int k = ax - 1;
-            const double dk = axis_comp(d, k);
-            if (!(fabs(dk) > 1e-6)) continue;
-            const double c = p[k] - axis_comp(o, k);
-            plane_occlusion_class(dk > 0.0 ? c : -c, fabs(dk), max_dist, bias, blocked,
-                                  undecided);
-            continue;
-        }
         const d3 n = mk(p[3], p[4], p[5]);
         const double denom = dot(n, d);
         if (!(fabs(denom) > 1e-6)) continue;
         const double num = dot(mk(p[0], p[1], p[2]) - o, n);
-        plane_occlusion_class(denom > 0.0 ? num : -num, fabs(denom), max_dist, bias, blocked,
-                              undecided);
+        const double A = denom > 0.0 ? num : -num, B = fabs(denom);
+        if (A < -1e-300 * B) continue;                        // t < 0 (no underflow to −0)
+        if (A >= max_dist * B * (1.0 + 1e-9)) continue;       // beyond the light
+        if (A > bias * B * (1.0 + 1e-9) && A < max_dist * B * (1.0 - 1e-9)) blocked = true;
+        else undecided = true;
     }
     return undecided ? 2 : (blocked ? 1 : 0);
 }
@@ -1042,7 +1001,6 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
     S.nt = P.nt;
     S.nl = nl;
     S.nb = nb;
-    S.pl_axis = P.pl_axis;
     S.orig = nb ? s_orig : nullptr;
     const int nchunks = (ns + 63) / 64;
 

@@ -42,7 +42,9 @@ __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParam
     bool run = x < P.width && yl < P.rows;
     if (P.redo) {  // uniform
         // fix-up pass of the wavefront renderer: only pixels with an incomplete sample tree,
-        // and workgroups without one leave before staging the scene
+        // and workgroups without one leave before staging the scene (all of them at once when
+        // no tree overflowed: one scalar load)
+        if (P.redo_any && *P.redo_any == 0u) return;
         if (run) {
             const size_t r0 = (static_cast<size_t>(yl) * P.width + x) * static_cast<size_t>(P.aa);
             bool any = false;
@@ -150,7 +152,6 @@ __device__ __forceinline__ SceneView global_view(const TraceParams& P) {
     S.np = P.np;
     S.nt = P.nt;
     S.nl = P.nl;
-    S.pl_axis = P.pl_axis;
     S.sph = P.sph;
     S.pl = P.pl;
     S.lt = P.lt;

@@ -25,65 +25,7 @@ struct SceneView {
     const double* bvh;       // triangle BVH (null: every triangle is tested)
     const int32_t* bvh_tri;
     int ns, np, nt, nl;
-    uint32_t pl_axis;        // TraceParams::pl_axis
 };
-
-// ------------------------------------------------------------------ axis-aligned planes
-// rt_scene_create marks a plane whose stored normal is exactly ±e_k (two components ±0, one ±1)
-// and whose point is within 2^1000 — every plane of the BASELINE scenes and all five of the
-// reference's own box (RaytracingEngine.cpp).  For a ray with |o|₁ ≤ 2^1020 and |d|₁ ≤ 2^100
-// (finite), Plane::Intersect (Shape.h:149-159) then reduces exactly:
-//  * denom = (n_x·d_x + n_y·d_y) + n_k·d_k: the first two products are ±0 (finite d), so
-//    denom = n_k·d_k whenever it is nonzero, and |denom| > 1e-6 ⇔ |d_k| > 1e-6;
-//  * num = (p − o)·n = n_k·c with c = p_k − o_k (the reference's own subtraction) whenever
-//    c ≠ 0 (the other two products are ±0: every p_i − o_i is finite);
-//  * t = num / denom = (n_k·c) / (n_k·d_k) = c / d_k bit for bit (IEEE division is odd in each
-//    operand).
-// The two dot products (ten FP64 operations) become one subtraction.  c == 0 (a ray starting
-// exactly on the plane) keeps the literal arithmetic: the sign of that zero num depends on the
-// other two products.  RT_FLAG_NO_AXIS_PLANES clears the codes (A/B and the parity tests).
-constexpr double kAxisOrigin = 0x1p1020, kAxisDir = 0x1p100;
-__device__ __forceinline__ int plane_axis(uint32_t bits, int i) {
-    return i < kAxisPlanes ? static_cast<int>((bits >> (2 * i)) & 3u) : 0;
-}
-__device__ __forceinline__ bool axis_ray_ok(d3 o, d3 d) {
-    return fabs(o.x) + fabs(o.y) + fabs(o.z) <= kAxisOrigin &&
-           fabs(d.x) + fabs(d.y) + fabs(d.z) <= kAxisDir;
-}
-// Component k (wave-uniform) of v: selects on a scalar condition (scalar branches into three
-// copies of the plane code cost the packet kernel 36 B/lane of spills)
-__device__ __forceinline__ double axis_comp(d3 v, int k) {
-    return k == 0 ? v.x : (k == 1 ? v.y : v.z);
-}
-// Plane::Intersect through the axis shortcut for a closest-hit search that holds `best`:
-// 0 = no hit that could replace it, 1 = hit at t (t >= 0, not provably >= best), 2 = c == 0,
-// the caller takes the literal path.  The division is skipped when its sign (|c| ≥ 2^-900 and
-// |d_k| ≤ 2^100: the quotient cannot round to −0) or its size (|c| > best·|d_k|·(1+2^-40), best
-// ≥ 2^-900 so the product is normal: the rounded quotient is ≥ best, which the reference's
-// strict '<' rejects) already decides it.
-constexpr double kAxisNoWin = 1.0 + 0x1.0p-40;
-__device__ __forceinline__ int axis_plane_t(double pk, double ok, double dk, bool found,
-                                            double best, double& t) {
-    if (!(fabs(dk) > 1e-6)) return 0;
-    const double c = pk - ok;
-    if (c == 0.0) return 2;
-    if ((c < 0.0) != (dk < 0.0) && fabs(c) >= 0x1p-900) return 0;
-    if (found && best >= 0x1p-900 && fabs(c) > (best * fabs(dk)) * kAxisNoWin) return 0;
-    t = c / dk;
-    return t >= 0.0 ? 1 : 0;
-}
-// computeTransmittance's classification of one plane from A = sign(denom)·num and B = |denom|
-// (t = A / B), decided without the division (1e-9 relative margin ≫ the FP64 rounding of the
-// quotient and the products): t < 0 or t ≥ maxDist clear, bias < t < maxDist blocked, anything
-// else (a near hit, a boundary) undecided.
-__device__ __forceinline__ void plane_occlusion_class(double A, double B, double max_dist,
-                                                      double bias, bool& blocked,
-                                                      bool& undecided) {
-    if (A < -1e-300 * B) return;                       // t < 0 (no underflow to −0)
-    if (A >= max_dist * B * (1.0 + 1e-9)) return;      // beyond the light
-    if (A > bias * B * (1.0 + 1e-9) && A < max_dist * B * (1.0 - 1e-9)) blocked = true;
-    else undecided = true;                             // near hit or on a boundary
-}
 
 struct Hit {
     double t;
@@ -233,24 +175,8 @@ __device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) 
             idx = i;
         }
     }
-    const bool axis_ok = S.pl_axis != 0 && axis_ray_ok(o, d);
     for (int i = 0; i < S.np; ++i) {
         const double* p = S.pl + kPlStride * i;
-        const int ax = plane_axis(S.pl_axis, i);  // uniform
-        bool literal = true;
-        if (ax != 0 && axis_ok) {
-            const int k = ax - 1;
-            double t;
-            const int r = axis_plane_t(p[k], axis_comp(o, k), axis_comp(d, k), found, best, t);
-            literal = r == 2;
-            if (r == 1 && (!found || t < best)) {
-                found = true;
-                best = t;
-                kind = 2;
-                idx = i;
-            }
-        }
-        if (!literal) continue;
         const d3 n = mk(p[3], p[4], p[5]);
         const double denom = dot(n, d);
         if (fabs(denom) > 1e-6) {
@@ -301,7 +227,6 @@ __device__ __forceinline__ SceneView stage_scene(const TraceParams& P, double* s
     S.np = P.np;
     S.nt = P.nt;
     S.nl = P.nl;
-    S.pl_axis = P.pl_axis;
     S.tri = P.tri;
     S.sph_mat = P.sph_mat;
     S.pl_mat = P.pl_mat;
@@ -459,27 +384,17 @@ __device__ __forceinline__ int occlusion_opaque(const SceneView& S, d3 o, d3 d, 
         if (t > bias + delta && t < max_dist - delta) blocked = true;
         else undecided = true;
     }
-    const bool axis_ok = S.pl_axis != 0 && axis_ray_ok(o, d);
     for (int i = 0; i < S.np; ++i) {
         const double* p = S.pl + kPlStride * i;
-        const int ax = plane_axis(S.pl_axis, i);  // uniform
-        if (ax != 0 && axis_ok) {
-            // A = sign(denom)·num = (d_k > 0 ? c : −c), B = |d_k| (c == 0: A = ±0, undecided
-            // either way, as the literal code decides it)
-            const int k = ax - 1;
-            const double dk = axis_comp(d, k);
-            if (!(fabs(dk) > 1e-6)) continue;
-            const double c = p[k] - axis_comp(o, k);
-            plane_occlusion_class(dk > 0.0 ? c : -c, fabs(dk), max_dist, bias, blocked,
-                                  undecided);
-            continue;
-        }
         const d3 n = mk(p[3], p[4], p[5]);
         const double denom = dot(n, d);
         if (!(fabs(denom) > 1e-6)) continue;
         const double num = dot(mk(p[0], p[1], p[2]) - o, n);
-        plane_occlusion_class(denom > 0.0 ? num : -num, fabs(denom), max_dist, bias, blocked,
-                              undecided);
+        const double A = denom > 0.0 ? num : -num, B = fabs(denom);
+        if (A < -1e-300 * B) continue;
+        if (A >= max_dist * B * (1.0 + 1e-9)) continue;
+        if (A > bias * B * (1.0 + 1e-9) && A < max_dist * B * (1.0 - 1e-9)) blocked = true;
+        else undecided = true;
     }
     return undecided ? -1 : (blocked ? 0 : 1);
 }

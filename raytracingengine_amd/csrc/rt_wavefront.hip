@@ -36,6 +36,9 @@ namespace lean {
 namespace {
 
 constexpr int kWfThreads = 256;
+#ifndef RT_WF_WG_ALLOC
+#define RT_WF_WG_ALLOC 1
+#endif
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {  // set bits below this lane
     return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32),
@@ -66,6 +69,19 @@ __device__ __forceinline__ uint32_t wf_tile_order(const TraceParams& P, uint32_t
     return (yl * P.width + x) * aa + s;
 }
 
+// A child at depth maxRecursion: TraceRay returns backgroundColor (Scene.h:132-134) — the node a
+// level kernel for that depth would write.
+__device__ __forceinline__ void write_leaf(const WfArena& A, uint32_t cid, d3 dir) {
+    const d3 v = sky(dir);
+    A.val[cid] = v.x;
+    A.val[A.cap + cid] = v.y;
+    A.val[2 * A.cap + cid] = v.z;
+    A.fw[cid] = 0.0;
+    A.rw[cid] = 0.0;
+    A.child[cid] = -1;
+    A.child[A.cap + cid] = -1;
+}
+
 // level kernels: 2 waves/SIMD, 3 in the lean build (213 → 168 VGPRs: glass 1.58 → 1.54 ms)
 #ifdef RT_LEAN_GENERIC
 constexpr int kWfLevelWaves = 3;
@@ -84,11 +100,27 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
     const int lane = threadIdx.x & 63;
     const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     const uint32_t aa = static_cast<uint32_t>(P.aa);
+    // the last shading level (depth maxRecursion − 1): its children are TraceRay calls at depth
+    // maxRecursion, which return the sky (Scene.h:132-134) — their node records are written
+    // here (value sky(direction), no children) instead of ray records for a level of their own
+    const bool leaves = level + 1 >= P.max_rec;
     Counts cnt{0u, 0u};
+#if RT_WF_WG_ALLOC
+    // Child slots of level + 1 are reserved with ONE device atomic per workgroup and iteration
+    // (the four waves' counts summed in LDS): a single counter hit by every wave of the chip
+    // serialises at memory, one atomic per wave cost the deep levels most of their time.
+    __shared__ uint32_t s_wtot[kWfThreads / 64], s_wbase;
+    const int wave = threadIdx.x >> 6;
+    // workgroup-uniform grid-stride loop (the barriers below): every wave of the workgroup runs
+    // every iteration, lanes past n idle (ballots below)
+    for (uint32_t b0 = blockIdx.x * kWfThreads; b0 < n; b0 += gridDim.x * kWfThreads) {
+        const uint32_t i = b0 + threadIdx.x;
+#else
     // wave-uniform grid-stride loop: all 64 lanes run every iteration (ballots below)
     for (uint32_t i0 = blockIdx.x * kWfThreads + (threadIdx.x & ~63u); i0 < n;
          i0 += gridDim.x * kWfThreads) {
         const uint32_t i = i0 + lane;
+#endif
         const bool active = i < n;
         const uint32_t id = base + (active ? (level == 0 ? wf_tile_order(P, i, aa) : i) : 0u);
         uint32_t root;
@@ -121,19 +153,36 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
         }
         const bool want_f = active && TREE && nd.hit && nd.refr;
         const bool want_r = active && nd.hit && nd.refl;
-        // one atomic per wave for all children of the wave
         const uint64_t bf = __ballot(want_f), br = __ballot(want_r);
         const uint32_t total = __builtin_popcountll(bf) + __builtin_popcountll(br);
         uint32_t wbase = 0;
+#if RT_WF_WG_ALLOC
+        // one atomic per workgroup for all children of its four waves, in wave order
+        if (lane == 0) s_wtot[wave] = total;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t sum = s_wtot[0] + s_wtot[1] + s_wtot[2] + s_wtot[3];
+            s_wbase = sum ? atomicAdd(&A.ctl->count[level + 1], sum) : 0u;
+        }
+        __syncthreads();
+        wbase = s_wbase;
+        for (int w = 0; w < wave; ++w) wbase += s_wtot[w];
+        __syncthreads();  // s_wtot / s_wbase are rewritten by the next iteration
+#else
+        // one atomic per wave for all children of the wave
         if (total) {
             if (lane == 0) wbase = atomicAdd(&A.ctl->count[level + 1], total);
             wbase = __shfl(wbase, 0, 64);
         }
+#endif
         int32_t cf = -1, cr = -1;
         bool lost = false;
         if (want_f) {
             const uint32_t cid = next + wbase + lane_prefix(bf);
-            if (cid < A.cap) {
+            if (cid < A.cap && leaves) {
+                write_leaf(A, cid, nd.fd);
+                cf = static_cast<int32_t>(cid);
+            } else if (cid < A.cap) {
                 const size_t r = cid - A.n0;
                 A.ray[r] = nd.fo.x;
                 A.ray[A.cap_r + r] = nd.fo.y;
@@ -150,7 +199,10 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
         if (want_r) {
             const uint32_t cid =
                 next + wbase + __builtin_popcountll(bf) + lane_prefix(br);
-            if (cid < A.cap) {
+            if (cid < A.cap && leaves) {
+                write_leaf(A, cid, nd.rd);
+                cr = static_cast<int32_t>(cid);
+            } else if (cid < A.cap) {
                 const size_t r = cid - A.n0;
                 A.ray[r] = nd.ro.x;
                 A.ray[A.cap_r + r] = nd.ro.y;
@@ -164,7 +216,10 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
                 lost = true;
             }
         }
-        if (lost) A.redo[root] = 1;  // the tree of this sample does not fit: per-pixel fix-up
+        if (lost) {  // the tree of this sample does not fit: per-pixel fix-up
+            A.redo[root] = 1;
+            A.ctl->lost = 1u;
+        }
         if (active) {
             A.val[id] = nd.value.x;
             A.val[A.cap + id] = nd.value.y;
@@ -241,7 +296,9 @@ hipError_t launch_levels(const TraceParams& p, const WfArena& A, size_t lds_byte
     if (g0 > 0)
         hipLaunchKernelGGL((wf_level_kernel<TREE, LDS>), dim3(g0), dim3(kWfThreads), lds, stream,
                            p, A, 0);
-    for (int k = 1; k <= max_level && gk > 0; ++k)
+    // levels 1 .. maxRecursion − 1 (the last shading level writes the depth-maxRecursion sky
+    // leaves itself)
+    for (int k = 1; k < max_level && gk > 0; ++k)
         hipLaunchKernelGGL((wf_level_kernel<TREE, LDS>), dim3(gk), dim3(kWfThreads), lds, stream,
                            p, A, k);
     for (int k = max_level - 1; k >= 1 && gf > 0; --k)
@@ -303,6 +360,7 @@ hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bo
     // build's own, rtamd::lean::launch_trace)
     TraceParams q = p;
     q.redo = A.redo;
+    q.redo_any = &A.ctl->lost;
 #ifdef RT_LEAN_GENERIC
     return rtamd::lean::launch_trace(q, path, false, lds, lds_bytes, stream);
 #else

@@ -13,6 +13,7 @@ namespace rtamd {
 struct WfCtl {
     uint32_t count[kMaxDepth + 2];
     uint32_t base[kMaxDepth + 2];
+    uint32_t lost;  // some sample's tree overflowed the arena (the fix-up pass has work)
 };
 
 // Node ids [0, n0) are the roots (pixel samples, row-local pixel * aa + sample); deeper nodes
