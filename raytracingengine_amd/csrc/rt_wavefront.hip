@@ -69,19 +69,6 @@ __device__ __forceinline__ uint32_t wf_tile_order(const TraceParams& P, uint32_t
     return (yl * P.width + x) * aa + s;
 }
 
-// A child at depth maxRecursion: TraceRay returns backgroundColor (Scene.h:132-134) — the node a
-// level kernel for that depth would write.
-__device__ __forceinline__ void write_leaf(const WfArena& A, uint32_t cid, d3 dir) {
-    const d3 v = sky(dir);
-    A.val[cid] = v.x;
-    A.val[A.cap + cid] = v.y;
-    A.val[2 * A.cap + cid] = v.z;
-    A.fw[cid] = 0.0;
-    A.rw[cid] = 0.0;
-    A.child[cid] = -1;
-    A.child[A.cap + cid] = -1;
-}
-
 // level kernels: 2 waves/SIMD, 3 in the lean build (213 → 168 VGPRs: glass 1.58 → 1.54 ms)
 #ifdef RT_LEAN_GENERIC
 constexpr int kWfLevelWaves = 3;
@@ -101,8 +88,8 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
     const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     const uint32_t aa = static_cast<uint32_t>(P.aa);
     // the last shading level (depth maxRecursion − 1): its children are TraceRay calls at depth
-    // maxRecursion, which return the sky (Scene.h:132-134) — their node records are written
-    // here (value sky(direction), no children) instead of ray records for a level of their own
+    // maxRecursion, which return the sky (Scene.h:132-134), so each node is folded right here —
+    // no child slots, no ray records, no level and no fold launch of their own
     const bool leaves = level + 1 >= P.max_rec;
     Counts cnt{0u, 0u};
 #if RT_WF_WG_ALLOC
@@ -153,6 +140,21 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
         }
         const bool want_f = active && TREE && nd.hit && nd.refr;
         const bool want_r = active && nd.hit && nd.refl;
+        if (leaves) {  // uniform: children at depth maxRecursion are the sky (Scene.h:132-134)
+            if (active) {
+                // the fold of this node with those children, in the reference's order
+                // (Scene.h:176-195): (local + refraction·fw) + reflection·rw
+                d3 v = nd.value;
+                if (want_f) v = v + sky(nd.fd) * nd.fw;
+                if (want_r) v = v + sky(nd.rd) * nd.rw;
+                A.val[id] = v.x;
+                A.val[A.cap + id] = v.y;
+                A.val[2 * A.cap + id] = v.z;
+                A.child[id] = -1;
+                A.child[A.cap + id] = -1;
+            }
+            continue;
+        }
         const uint64_t bf = __ballot(want_f), br = __ballot(want_r);
         const uint32_t total = __builtin_popcountll(bf) + __builtin_popcountll(br);
         uint32_t wbase = 0;
@@ -179,10 +181,7 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
         bool lost = false;
         if (want_f) {
             const uint32_t cid = next + wbase + lane_prefix(bf);
-            if (cid < A.cap && leaves) {
-                write_leaf(A, cid, nd.fd);
-                cf = static_cast<int32_t>(cid);
-            } else if (cid < A.cap) {
+            if (cid < A.cap) {
                 const size_t r = cid - A.n0;
                 A.ray[r] = nd.fo.x;
                 A.ray[A.cap_r + r] = nd.fo.y;
@@ -199,10 +198,7 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
         if (want_r) {
             const uint32_t cid =
                 next + wbase + __builtin_popcountll(bf) + lane_prefix(br);
-            if (cid < A.cap && leaves) {
-                write_leaf(A, cid, nd.rd);
-                cr = static_cast<int32_t>(cid);
-            } else if (cid < A.cap) {
+            if (cid < A.cap) {
                 const size_t r = cid - A.n0;
                 A.ray[r] = nd.ro.x;
                 A.ray[A.cap_r + r] = nd.ro.y;
@@ -296,12 +292,12 @@ hipError_t launch_levels(const TraceParams& p, const WfArena& A, size_t lds_byte
     if (g0 > 0)
         hipLaunchKernelGGL((wf_level_kernel<TREE, LDS>), dim3(g0), dim3(kWfThreads), lds, stream,
                            p, A, 0);
-    // levels 1 .. maxRecursion − 1 (the last shading level writes the depth-maxRecursion sky
-    // leaves itself)
+    // levels 1 .. maxRecursion − 1 (depth maxRecursion is folded in by the last of them)
     for (int k = 1; k < max_level && gk > 0; ++k)
         hipLaunchKernelGGL((wf_level_kernel<TREE, LDS>), dim3(gk), dim3(kWfThreads), lds, stream,
                            p, A, k);
-    for (int k = max_level - 1; k >= 1 && gf > 0; --k)
+    // folds of levels maxRecursion − 2 .. 1 (the last shading level folded its nodes itself)
+    for (int k = max_level - 2; k >= 1 && gf > 0; --k)
         hipLaunchKernelGGL(wf_fold_kernel, dim3(gf), dim3(kWfThreads), 0, stream, A, k);
     const size_t npx = static_cast<size_t>(p.rows) * p.width;
     if (npx > 0)
