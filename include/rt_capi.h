@@ -165,6 +165,8 @@ typedef struct rt_render_opts {
 #define RT_FLAG_PIPELINE 0x10      /* rt_render_gather: gather + assembly on the communicator's
                                       own stream, overlapping the next frame's render (two
                                       frame slots); rt_comm_synchronize waits for the frame   */
+#define RT_FLAG_NO_TILE_ORDER 0x20 /* ablation: the packet kernel's default tile order instead
+                                      of costliest tiles first (the image is the same)        */
 
 /* Fills opts with the reference defaults: max_recursion 10, bias 1e-3, tonemap ACES,
  * full image, seed 0x5EED, no flags. */
@@ -343,6 +345,14 @@ rt_status rt_debug_vec_ops(rt_context* ctx, const double* v, size_t n, double* o
 rt_status rt_debug_assemble_rows(rt_context* ctx, const void* gathered, size_t row_bytes,
                                  uint32_t height, uint32_t block, uint32_t n, uint32_t max_rows,
                                  void* image);
+
+/* Test hook: the packet kernel's costliest-first tile order of `scene` seen from cam->position
+ * (rt_capi.cpp tile_order): *tiles / *waves receive the launch shape (0 when the camera has no
+ * order state), `order` (capacity `tiles`) the dispatch order once built, `cost` (capacity
+ * tiles*waves) the recorded wave durations (100 MHz ticks); either may be NULL. */
+rt_status rt_debug_tile_order(rt_context* ctx, const rt_scene* scene, const rt_camera* cam,
+                              uint32_t* order, uint32_t* cost, size_t capacity, uint32_t* tiles,
+                              uint32_t* waves, int* state);
 
 #ifdef __cplusplus
 } /* extern "C" */

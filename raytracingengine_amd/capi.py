@@ -30,6 +30,7 @@ RT_FLAG_TIME_KERNEL = 0x2
 RT_FLAG_GENERIC_KERNEL = 0x4
 RT_FLAG_NO_BVH = 0x8
 RT_FLAG_PIPELINE = 0x10
+RT_FLAG_NO_TILE_ORDER = 0x20
 RT_OUT_HDR64, RT_OUT_HDR32, RT_OUT_LDR = 0x1, 0x2, 0x4
 RT_COMM_ID_BYTES = 128
 
@@ -40,7 +41,7 @@ EXPORTED = [
     "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
     "rt_render_multi", "rt_comm_unique_id", "rt_comm_create", "rt_comm_create_all",
     "rt_comm_create_local", "rt_comm_destroy", "rt_comm_info", "rt_render_gather", "rt_render_gather_all",
-    "rt_comm_timing", "rt_comm_synchronize", "rt_debug_assemble_rows",
+    "rt_comm_timing", "rt_comm_synchronize", "rt_debug_assemble_rows", "rt_debug_tile_order",
     "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
     "rt_debug_f64_ops", "rt_debug_vec_ops", "rt_queue_create", "rt_queue_destroy",
     "rt_queue_submit", "rt_queue_wait", "rt_queue_synchronize",
@@ -143,6 +144,7 @@ def load_library(path: str = LIB_PATH):
         "rt_queue_submit": [vp, vp, vp, vp, vp, vp, vp, vp],
         "rt_queue_wait": [vp, ctypes.c_uint64],
         "rt_queue_synchronize": [vp],
+        "rt_debug_tile_order": [vp, vp, vp, vp, vp, ctypes.c_size_t, vp, vp, vp],
         "rt_debug_assemble_rows": [vp, vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
                                    ctypes.c_uint32, ctypes.c_uint32, vp],
     }.items():
@@ -347,6 +349,24 @@ class DeviceScene:
         _check(_lib.rt_intersect_rays(self.ctx.handle, self._h, rays.ctypes.data, rays.shape[0],
                                       out.ctypes.data))
         return out
+
+    def debug_tile_order(self):
+        """The packet kernel's tile-order state for this scene's camera (rt_debug_tile_order):
+        (state, order[tiles] or None, cost[tiles, waves] or None)."""
+        tiles, waves, state = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int()
+        _check(_lib.rt_debug_tile_order(self.ctx.handle, self._h, self.camera.ctypes.data, None,
+                                        None, 0, ctypes.byref(tiles), ctypes.byref(waves),
+                                        ctypes.byref(state)))
+        if state.value == 0:
+            return 0, None, None
+        n, w = tiles.value, waves.value
+        order = np.empty(n, np.uint32)
+        cost = np.empty(n * w, np.uint32)
+        _check(_lib.rt_debug_tile_order(self.ctx.handle, self._h, self.camera.ctypes.data,
+                                        order.ctypes.data if state.value == 2 else None,
+                                        cost.ctypes.data, cost.size, ctypes.byref(tiles),
+                                        ctypes.byref(waves), ctypes.byref(state)))
+        return state.value, (order if state.value == 2 else None), cost.reshape(n, w)
 
     def render_device(self, d_hdr64: int | None, d_hdr32: int | None, d_ldr: int | None,
                       opts: RenderOpts):

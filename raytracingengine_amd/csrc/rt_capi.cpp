@@ -249,7 +249,52 @@ rt_status packet_publish_slot(rt_context* ctx, const rt_scene* sc, TraceParams& 
                                                      (ep % kPkPubSlots) * slot);
     return RT_OK;
 }
-rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
+// Costliest tiles first (rt_packet.hip packet_order_kernel): the launch that creates a camera's
+// packet image also records every wave's duration; the next launch of the same shape sorts the
+// tiles by them (one small kernel, once) and every later one dispatches the costliest tiles
+// first, so the cheapest fill the partly idle end of the launch.  The order only permutes which
+// workgroup renders which tile: every pixel is computed by the same instructions, so images do
+// not change (RT_FLAG_NO_TILE_ORDER: the default order, for A/B runs and the tests).  `*rec`
+// receives the entry whose recording launch enqueue_render marks complete.
+rt_status tile_order(rt_context* ctx, rt_scene::PkImage& im, TraceParams& p, int flags,
+                     rt_scene::PkImage::TileOrder** rec) {
+    *rec = nullptr;
+    if (flags & RT_FLAG_NO_TILE_ORDER) return RT_OK;
+    auto& o = im.ord;
+    uint32_t gx, gy, waves;
+    packet_grid(p, gx, gy, waves);
+    const uint32_t key[8] = {gx, gy, waves, p.width, p.height, p.rows, p.row0,
+                             (p.row_block << 16) ^ p.row_stride};
+    const uint32_t tiles = gx * gy;
+    if (o.state == 0 || std::memcmp(o.key, key, sizeof key) != 0) {  // record this launch
+        RT_HIP(o.cost.ensure(sizeof(uint32_t) * tiles * waves));
+        if (!o.recorded) RT_HIP(hipEventCreateWithFlags(&o.recorded, hipEventDisableTiming));
+        std::memcpy(o.key, key, sizeof key);
+        o.state = 1;
+        p.tile_cost = static_cast<uint32_t*>(o.cost.ptr);
+        *rec = &o;
+        return RT_OK;
+    }
+    if (o.state == 1) {  // build the order (after the recording launch, on whatever stream)
+        RT_HIP(o.keys.ensure(sizeof(uint32_t) * tiles));
+        RT_HIP(o.order.ensure(sizeof(uint32_t) * tiles));
+        if (!o.built) RT_HIP(hipEventCreateWithFlags(&o.built, hipEventDisableTiming));
+        RT_HIP(hipStreamWaitEvent(ctx->stream, o.recorded, 0));
+        RT_HIP(launch_packet_order(static_cast<const uint32_t*>(o.cost.ptr), gx, gy, waves,
+                                   static_cast<uint32_t*>(o.keys.ptr),
+                                   static_cast<uint32_t*>(o.order.ptr), ctx->stream));
+        RT_HIP(hipEventRecord(o.built, ctx->stream));
+        o.state = 2;
+    } else {
+        RT_HIP(hipStreamWaitEvent(ctx->stream, o.built, 0));  // built on another stream
+    }
+    p.tile_order = static_cast<const uint32_t*>(o.order.ptr);
+    return RT_OK;
+}
+
+rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p, int flags,
+                       rt_scene::PkImage::TileOrder** rec) {
+    *rec = nullptr;
     for (auto& im : sc->pk_images) {
         if (std::memcmp(im.cam, p.cam_pos, sizeof im.cam) != 0) continue;
         if (!im.done && im.stream != ctx->stream) {
@@ -259,7 +304,7 @@ rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
             else return hip_fail(q, "hipEventQuery");
         }
         p.pk_image = static_cast<const double*>(im.buf.ptr);
-        return RT_OK;
+        return tile_order(ctx, im, p, flags, rec);
     }
     auto& seen = sc->pk_seen;
     auto it = std::find_if(seen.begin(), seen.end(), [&](const std::array<double, 3>& c) {
@@ -287,7 +332,7 @@ rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p) {
         return hip_fail(e, "packet image setup");
     }
     p.pk_image = static_cast<const double*>(im.buf.ptr);
-    return RT_OK;
+    return tile_order(ctx, im, p, flags, rec);
 }
 
 // Whether a render of this TraceRay shape takes the breadth-first path, whose arena (ctx->wf,
@@ -345,8 +390,9 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
     const bool packet = path == kPathDirect && !(flags & RT_FLAG_GENERIC_KERNEL) &&
                         p.ns <= packet_max_spheres() &&
                         packet_lds_bytes(p.ns, p.np, p.nl) <= ctx->lds_limit;
+    rt_scene::PkImage::TileOrder* rec = nullptr;  // set: this launch records wave durations
     if (packet) {
-        st = packet_image(ctx, sc, p);
+        st = packet_image(ctx, sc, p, flags, &rec);
         if (st != RT_OK) return st;
     }
     // generic kernels without triangle / area-light code for scenes that use neither
@@ -383,6 +429,7 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
         }
     }
     if (!wavefront) RT_HIP(launch(p, false));
+    if (rec) RT_HIP(hipEventRecord(rec->recorded, ctx->stream));
     if (flags & RT_FLAG_TIME_KERNEL) {
         RT_HIP(hipEventRecord(ev.second, ctx->stream));
         ctx->pending.push_back(ev);
@@ -394,6 +441,7 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
         pc.out32 = nullptr;
         pc.ldr = nullptr;
         pc.counters = static_cast<unsigned long long*>(ctx->counters.ptr);
+        pc.tile_cost = nullptr;  // the durations are the image launch's
         RT_HIP(launch(pc, true));
     }
     return RT_OK;
@@ -631,6 +679,11 @@ rt_status rt_scene_destroy(rt_scene* sc) {
     for (auto& im : sc->pk_images) {
         im.buf.release();
         if (im.ready) (void)hipEventDestroy(im.ready);
+        im.ord.cost.release();
+        im.ord.keys.release();
+        im.ord.order.release();
+        if (im.ord.recorded) (void)hipEventDestroy(im.ord.recorded);
+        if (im.ord.built) (void)hipEventDestroy(im.ord.built);
     }
     delete sc;
     return RT_OK;
@@ -840,6 +893,37 @@ rt_status rt_debug_f64_ops(rt_context* ctx, const double* x, const double* y, si
     RT_HIP(launch_debug_f64(dx, dy, n, dout, ctx->stream));
     RT_HIP(hipMemcpyAsync(out, dout, 5 * n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+rt_status rt_debug_tile_order(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
+                              uint32_t* order, uint32_t* cost, size_t capacity, uint32_t* tiles,
+                              uint32_t* waves, int* state) {
+    if (!ctx || !sc || !cam || !tiles || !waves || !state)
+        return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_debug_tile_order");
+    *tiles = *waves = 0;
+    *state = 0;
+    DeviceGuard g(ctx->device);
+    RT_HIP(hipDeviceSynchronize());
+    for (const auto& im : sc->pk_images) {
+        if (std::memcmp(im.cam, cam->position, sizeof im.cam) != 0) continue;
+        const auto& o = im.ord;
+        *state = o.state;
+        if (o.state == 0) return RT_OK;
+        *tiles = o.key[0] * o.key[1];
+        *waves = o.key[2];
+        if (order && o.state == 2) {
+            if (capacity < *tiles) return fail(RT_ERR_INVALID_ARG, "order capacity too small");
+            RT_HIP(hipMemcpy(order, o.order.ptr, sizeof(uint32_t) * *tiles, hipMemcpyDeviceToHost));
+        }
+        if (cost) {
+            if (capacity < size_t(*tiles) * *waves)
+                return fail(RT_ERR_INVALID_ARG, "cost capacity too small");
+            RT_HIP(hipMemcpy(cost, o.cost.ptr, sizeof(uint32_t) * *tiles * *waves,
+                             hipMemcpyDeviceToHost));
+        }
+        return RT_OK;
+    }
     return RT_OK;
 }
 

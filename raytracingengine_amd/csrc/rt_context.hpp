@@ -103,6 +103,15 @@ struct rt_scene {
         hipEvent_t ready = nullptr;
         hipStream_t stream = nullptr;
         bool done = false;
+        // Costliest-first tile order of the packet kernel for this camera (rt_capi.cpp
+        // tile_order): the wave durations one launch records, then the order built from them,
+        // for launches of the same shape (grid, rows) — state 0 none, 1 recorded, 2 ordered.
+        struct TileOrder {
+            uint32_t key[8] = {};  // gx gy waves width height rows row0 row_block|row_stride
+            int state = 0;
+            rtamd::DeviceBuffer cost, keys, order;
+            hipEvent_t recorded = nullptr, built = nullptr;
+        } ord;
     };
     mutable std::vector<PkImage> pk_images;
     mutable std::vector<std::array<double, 3>> pk_seen;  // cameras rendered once, no image yet

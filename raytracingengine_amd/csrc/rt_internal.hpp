@@ -83,6 +83,11 @@ struct TraceParams {
     const double* sph_bnd;
     // generic kernels with `redo`: 0 here means no sample overflowed, every workgroup leaves
     const uint32_t* redo_any;
+    // packet kernel: the tile each workgroup renders, by dispatch position (costliest first,
+    // packet_order_kernel), or null for the default bottom-up order; and, when set, where each
+    // wave records its duration (per tile and wave) for the next order
+    const uint32_t* tile_order;
+    uint32_t* tile_cost;
 };
 
 // Host: the spatial sphere chunks of the packet kernel's culls (rt_bvh.cpp): perm[sorted] =
@@ -111,6 +116,11 @@ hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specu
                                 hipStream_t stream);
 size_t packet_lds_bytes(int ns, int np, int nl);
 hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t stream);
+// The packet kernel's launch shape for p (grid of workgroups, waves per workgroup), and the
+// costliest-first tile order built from the wave durations a launch of that shape recorded.
+void packet_grid(const TraceParams& p, uint32_t& gx, uint32_t& gy, uint32_t& waves);
+hipError_t launch_packet_order(const uint32_t* cost, uint32_t gx, uint32_t gy, uint32_t waves,
+                               uint32_t* keys, uint32_t* order, hipStream_t stream);
 int packet_max_spheres();
 hipError_t launch_trace_rays(const TraceParams& p, int path, bool count, const double* rays,
                              size_t n, double* out, hipStream_t stream);

@@ -924,6 +924,23 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
     constexpr bool kNoPL = (FEAT & kFeatNoPL) != 0;  // the launcher checked P.np == P.nl == 0
+    // The tile this workgroup renders.  Results do not depend on the order; the tail of the
+    // launch does.  Default: rows bottom-up (scenes lit from above put the shadow-ray work on
+    // the floor and little on the sky / back wall, so the cheap top rows fill the partly idle
+    // end: C3 -9 %, C5 -1 %, C2/C4 within ±1 %; centre-out and edges-in orders measured worse).
+    // With a tile order (costliest first, from the wave durations of an earlier launch of this
+    // scene, camera and shape: packet_order_kernel) the cheapest tiles fill the end instead.
+    const uint32_t lin = blockIdx.y * gridDim.x + blockIdx.x;  // dispatch position
+    uint32_t tbx = blockIdx.x, tby = gridDim.y - 1 - blockIdx.y;
+    if (P.tile_order) {
+        const uint32_t t = P.tile_order[lin];
+        tbx = t % gridDim.x;
+        tby = t / gridDim.x;
+    }
+    // the recording launch (the general variant, rt_capi.cpp tile_order): each wave's start
+    uint64_t t_start = 0;
+    if constexpr (MULTI)
+        if (P.tile_cost) t_start = __builtin_amdgcn_s_memrealtime();
     const int ns = P.ns, np = kNoPL ? 0 : P.np, nl = kNoPL ? 0 : P.nl, nb = pk_chunk_bounds(ns),
               nsb = ns + nb;
     double* s_sph = smem;                                         // 32·nsb bytes
@@ -955,7 +972,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
         uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
         const int nw = static_cast<int>(pk_image_bytes(ns, np, nl) / 4);  // a multiple of 4
         const uint32_t ep = P.pk_epoch;
-        const uint32_t wg = blockIdx.y * gridDim.x + blockIdx.x;
+        const uint32_t wg = lin;
         bool have = false;
         if (wg >= P.pk_pub_first) {
             int ok = 1;
@@ -1005,14 +1022,8 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
     const int nchunks = (ns + 63) / 64;
 
     const int lane = tid & 63, wave = tid >> 6;
-    const uint32_t x = blockIdx.x * (kPkW * kWgWavesX) + (wave % kWgWavesX) * kPkW + (lane % kPkW);
-    // Workgroup rows are dispatched bottom-up.  Results do not depend on the order; the tail of
-    // the launch does: scenes lit from above put the shadow-ray work on the floor (bottom) and
-    // little on the sky / back wall (top), so finishing on the top rows leaves the cheap
-    // workgroups for the partly idle end (C3 -9 %, C5 -1 %, C2/C4 within ±1 %; centre-out and
-    // edges-in orders measured worse).
-    const uint32_t by = gridDim.y - 1 - blockIdx.y;
-    const uint32_t yl = by * (kPkH * WGY) + (wave / kWgWavesX) * kPkH + (lane / kPkW);
+    const uint32_t x = tbx * (kPkW * kWgWavesX) + (wave % kWgWavesX) * kPkW + (lane % kPkW);
+    const uint32_t yl = tby * (kPkH * WGY) + (wave / kWgWavesX) * kPkH + (lane / kPkW);
     const bool valid = x < P.width && yl < P.rows;
     // lanes past the image edge trace a clamped in-image ray: they take part in the packet
     // reductions (a superset bound is still conservative) and write nothing.
@@ -1206,6 +1217,13 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
             atomicAdd(P.counters + 1, static_cast<unsigned long long>(sh));
         }
     }
+    if constexpr (MULTI) {
+        if (P.tile_cost && lane == 0) {  // this wave's duration (100 MHz wall clock), per tile
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+            P.tile_cost[(tby * gridDim.x + tbx) * (kWgWavesX * WGY) + wave] =
+                static_cast<uint32_t>(t_end - t_start);
+        }
+    }
 }
 
 #ifdef RT_PACKET_PROBE
@@ -1225,6 +1243,97 @@ hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t st
 }
 
 int packet_max_spheres() { return 16 * 64; }
+
+void packet_grid(const TraceParams& p, uint32_t& gx, uint32_t& gy, uint32_t& waves) {
+    const size_t lds = pk_image_bytes(p.ns, p.np, p.nl);
+    const uint32_t wgy = 10 * lds <= kLdsPerCu ? 1u : 2u;  // launch_packet_variant's choice
+    gx = (p.width + kPkW * kWgWavesX - 1) / (kPkW * kWgWavesX);
+    gy = (p.rows + kPkH * wgy - 1) / (kPkH * wgy);
+    waves = kWgWavesX * wgy;
+}
+
+// Costliest tiles first: the tile order of the next launches from the wave durations one launch
+// recorded (tile_cost, `waves` per tile).  One workgroup: a tile's cost is its slowest wave's
+// (a workgroup holds its slots until then), binned into 16 levels of the largest cost; the bins
+// are dispatched costliest first, and inside a bin the tiles keep the default (bottom-up) order,
+// so tiles of similar cost stay spatially together (a fully cost-sorted order was 3.6 % slower on
+// C2, whose tiles cost nearly the same).  Every key is read once and kept (`keys`), so the
+// output is a permutation of the tiles even if another launch rewrites the costs meanwhile.
+constexpr int kOrderBins = 16;
+__global__ __launch_bounds__(1024) void packet_order_kernel(const uint32_t* cost, uint32_t gx,
+                                                            uint32_t gy, uint32_t waves,
+                                                            uint32_t* keys, uint32_t* order) {
+    __shared__ uint32_t s_max, s_cnt[kOrderBins];
+    const uint32_t tid = threadIdx.x, tiles = gx * gy;
+    if (tid == 0) s_max = 0;
+    if (tid < kOrderBins) s_cnt[tid] = 0;
+    __syncthreads();
+    uint32_t m = 0;
+    for (uint32_t i = tid; i < tiles; i += blockDim.x) {
+        uint32_t c = 0;
+        for (uint32_t w = 0; w < waves; ++w) c = max(c, cost[i * waves + w]);
+        keys[i] = c;
+        m = max(m, c);
+    }
+    atomicMax(&s_max, m);
+    __syncthreads();
+    const uint64_t top = static_cast<uint64_t>(s_max) + 1;
+    for (uint32_t i = tid; i < tiles; i += blockDim.x) {
+        const uint64_t bin = static_cast<uint64_t>(keys[i]) * kOrderBins / top;  // < kOrderBins
+        const uint32_t key = kOrderBins - 1 - static_cast<uint32_t>(bin);        // 0: costliest
+        keys[i] = key;
+        atomicAdd(&s_cnt[key], 1u);
+    }
+    __syncthreads();
+    if (tid >= 64) return;
+    // Narrow distributions keep the default order: when the median tile costs at least a
+    // quarter of the costliest (C2: ~0.4), costliest-first was slower (C2 +3 %, MI355X); wide
+    // ones (C3-C5: a few tiles at 10-35x the median) gain 4-10 %.
+    uint32_t acc = 0;
+    int median_bin = 0;  // cost bin (0 cheapest) holding the median tile
+    for (int b = kOrderBins - 1; b >= 0; --b) {  // keys from cheapest (kOrderBins - 1) up
+        acc += s_cnt[b];
+        if (2 * acc >= tiles) {
+            median_bin = kOrderBins - 1 - b;
+            break;
+        }
+    }
+    const bool narrow = median_bin >= kOrderBins / 4;
+    // one wave scatters the tiles in default dispatch order (bottom-up rows), stably per bin:
+    // lane b < kOrderBins holds bin b's cursor
+    uint32_t cur = 0;
+    for (int b = 0; b < kOrderBins; ++b)
+        if (static_cast<int>(tid) > b) cur += s_cnt[b];
+    if (narrow) {
+        for (uint32_t lin = tid; lin < tiles; lin += 64) order[lin] = (gy - 1 - lin / gx) * gx + lin % gx;
+        return;
+    }
+    const uint64_t below = (1ull << tid) - 1ull;
+    for (uint32_t c0 = 0; c0 < tiles; c0 += 64) {
+        const uint32_t lin = c0 + tid;
+        const bool ok = lin < tiles;
+        uint32_t tile = 0, key = kOrderBins;
+        if (ok) {
+            tile = (gy - 1 - lin / gx) * gx + lin % gx;
+            key = keys[tile];
+        }
+        for (int b = 0; b < kOrderBins; ++b) {
+            const uint64_t mk_ = __ballot(key == static_cast<uint32_t>(b));
+            if (!mk_) continue;  // uniform
+            const uint32_t base = __builtin_amdgcn_readlane(cur, b);
+            if (key == static_cast<uint32_t>(b))
+                order[base + __builtin_popcountll(mk_ & below)] = tile;
+            if (static_cast<int>(tid) == b) cur += __builtin_popcountll(mk_);
+        }
+    }
+}
+
+hipError_t launch_packet_order(const uint32_t* cost, uint32_t gx, uint32_t gy, uint32_t waves,
+                               uint32_t* keys, uint32_t* order, hipStream_t stream) {
+    hipLaunchKernelGGL(packet_order_kernel, dim3(1), dim3(1024), 0, stream, cost, gx, gy, waves,
+                       keys, order);
+    return hipGetLastError();
+}
 #endif
 
 
@@ -1236,8 +1345,10 @@ static void launch_packet_shape(const TraceParams& p, bool count, size_t lds, hi
     // the single-sample variant keeps no accumulator live across the trace (AA = 1, the
     // reference default for a preview and the bench's configuration); counting passes use the
     // general one
+    // (a launch that records its wave durations for the tile order takes the general variant:
+    // the single-sample one carries no recording code)
     if (count) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, true, true, WGY>), grid, block, lds, stream, p);
-    else if (p.aa == 1) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, false, WGY>), grid, block, lds, stream, p);
+    else if (p.aa == 1 && !p.tile_cost) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, false, WGY>), grid, block, lds, stream, p);
     else hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, true, WGY>), grid, block, lds, stream, p);
 }
 

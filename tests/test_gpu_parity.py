@@ -816,3 +816,41 @@ def test_edge_axis_planes_scene_vs_oracle(ctx, oracle, flags):
     ref, nt, ns = oracle.render(sc)
     assert np.array_equal(out["hdr64"], ref)
     assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)
+
+
+# ------------------------------------------------------------------ costliest-first tile order
+@pytest.mark.parametrize("name,w,h", [("c2", 1920, 1080), ("c3", 1920, 1080), ("c5", 960, 540),
+                                      ("c4", 1000, 600)])
+def test_tile_order_is_a_permutation_and_keeps_the_image(ctx, name, w, h):
+    """rt_capi.cpp tile_order: the render that creates a camera's packet image records every
+    wave's duration, the next one builds the dispatch order (rt_packet.hip packet_order_kernel)
+    and renders by it.  The order is a permutation of the tiles (every tile rendered exactly
+    once) and the image is bit-identical to the unordered renders."""
+    sc = make_config(name, w, h)
+    ds = ctx.scene(sc)
+    try:
+        first = ds.render(hdr64=True)                       # publish slot, default order
+        assert ds.debug_tile_order()[0] == 0
+        second = ds.render(hdr64=True)                      # image created, durations recorded
+        st, order, cost = ds.debug_tile_order()
+        assert st == 1 and order is None and (cost > 0).all()
+        third = ds.render(hdr64=True)                       # order built and used
+        st, order, cost = ds.debug_tile_order()
+        assert st == 2
+        assert np.array_equal(np.sort(order), np.arange(order.size, dtype=np.uint32))
+        tile = cost.max(axis=1).astype(np.float64)
+        print(f"TILECOST {name} {w}x{h}: tiles {tile.size} median {np.median(tile):.0f} "
+              f"p99 {np.percentile(tile, 99):.0f} max {tile.max():.0f} (10 ns ticks); "
+              f"order default {bool(np.array_equal(order[:8], _default_order(order.size, w)[:8]))}")
+        unordered = ds.render(hdr64=True, flags=capi.RT_FLAG_NO_TILE_ORDER)
+    finally:
+        ds.close()
+    for img in (second, third, unordered):
+        assert np.array_equal(img["hdr64"], first["hdr64"])
+
+
+def _default_order(tiles, w):
+    gx = (w + 15) // 16
+    gy = tiles // gx
+    lin = np.arange(tiles)
+    return (gy - 1 - lin // gx) * gx + lin % gx

@@ -1,6 +1,6 @@
 """Dev tool: packet-kernel time only (no bit-exactness check), for ablation builds whose images
 are deliberately wrong.  RTAMD_LIB selects the build."""
-import sys, json, time
+import os, sys, json, time
 sys.path.insert(0, '.')
 import torch
 from raytracingengine_amd import capi
@@ -13,7 +13,7 @@ for name in sys.argv[1:] or ["c2"]:
     W, H = sc.camera.width, sc.camera.height
     hdr = torch.empty(W * H * 3, dtype=torch.float64, device="cuda")
     ldr = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
-    o = capi.default_opts(tonemap=1, flags=capi.RT_FLAG_TIME_KERNEL)
+    o = capi.default_opts(tonemap=1, flags=capi.RT_FLAG_TIME_KERNEL | int(os.environ.get("AB_FLAGS", "0")))
     t_end = time.perf_counter() + 0.05   # the GPU's clock ramp (tools/clock_ramp.py)
     while time.perf_counter() < t_end:
         for _ in range(8):
