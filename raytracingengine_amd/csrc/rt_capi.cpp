@@ -279,13 +279,18 @@ rt_status tile_order(rt_context* ctx, rt_scene::PkImage& im, TraceParams& p, int
         RT_HIP(o.keys.ensure(sizeof(uint32_t) * tiles));
         RT_HIP(o.order.ensure(sizeof(uint32_t) * tiles));
         if (!o.built) RT_HIP(hipEventCreateWithFlags(&o.built, hipEventDisableTiming));
+        if (!o.verdict) RT_HIP(hipHostMalloc(reinterpret_cast<void**>(&o.verdict), sizeof(uint32_t)));
+        __atomic_store_n(o.verdict, 0u, __ATOMIC_RELAXED);
         RT_HIP(hipStreamWaitEvent(ctx->stream, o.recorded, 0));
         RT_HIP(launch_packet_order(static_cast<const uint32_t*>(o.cost.ptr), gx, gy, waves,
                                    static_cast<uint32_t*>(o.keys.ptr),
-                                   static_cast<uint32_t*>(o.order.ptr), ctx->stream));
+                                   static_cast<uint32_t*>(o.order.ptr), o.verdict, ctx->stream));
         RT_HIP(hipEventRecord(o.built, ctx->stream));
         o.state = 2;
     } else {
+        // a narrow cost distribution keeps the default order: no table at all (the verdict is
+        // only ever read as "narrow" once the order kernel has written it)
+        if (__atomic_load_n(o.verdict, __ATOMIC_RELAXED) == 1u) return RT_OK;
         RT_HIP(hipStreamWaitEvent(ctx->stream, o.built, 0));  // built on another stream
     }
     p.tile_order = static_cast<const uint32_t*>(o.order.ptr);
@@ -684,6 +689,7 @@ rt_status rt_scene_destroy(rt_scene* sc) {
         im.ord.order.release();
         if (im.ord.recorded) (void)hipEventDestroy(im.ord.recorded);
         if (im.ord.built) (void)hipEventDestroy(im.ord.built);
+        if (im.ord.verdict) (void)hipHostFree(im.ord.verdict);
     }
     delete sc;
     return RT_OK;

@@ -111,6 +111,9 @@ struct rt_scene {
             int state = 0;
             rtamd::DeviceBuffer cost, keys, order;
             hipEvent_t recorded = nullptr, built = nullptr;
+            // pinned host word the order kernel fills: 0 not yet, 1 narrow (keep the default
+            // order, no table), 2 dispatch by the table
+            uint32_t* verdict = nullptr;
         } ord;
     };
     mutable std::vector<PkImage> pk_images;

@@ -120,7 +120,8 @@ hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t st
 // costliest-first tile order built from the wave durations a launch of that shape recorded.
 void packet_grid(const TraceParams& p, uint32_t& gx, uint32_t& gy, uint32_t& waves);
 hipError_t launch_packet_order(const uint32_t* cost, uint32_t gx, uint32_t gy, uint32_t waves,
-                               uint32_t* keys, uint32_t* order, hipStream_t stream);
+                               uint32_t* keys, uint32_t* order, uint32_t* verdict,
+                               hipStream_t stream);
 int packet_max_spheres();
 hipError_t launch_trace_rays(const TraceParams& p, int path, bool count, const double* rays,
                              size_t n, double* out, hipStream_t stream);

@@ -120,11 +120,17 @@ __device__ __forceinline__ d3 lane_d3(d3 v, int l) {
     return mk(lane_d(v.x, l), lane_d(v.y, l), lane_d(v.z, l));
 }
 
+// A sphere of the packet image (LDS): kPkSph doubles — cx cy cz r², the camera-cone terms as 8
+// floats (cone_terms: vx vy vz q | rr dv slack r, r = the culling radius rounded up), the
+// camera-ray constant c = oc·oc − r² with oc = cam − C (Shape.h:73,77; the candidates form oc
+// again, the same three subtractions), 8 B of padding.  The lane-parallel culls read record `lane` with ds_read_b128: at an 80-B stride the
+// 16 lanes of every ds_read_b128 lane group start on distinct 16-B slots of the 256-B bank row
+// (20·lane mod 64 distinct), where the former 32-B records (plus a separate radius array) gave
+// 2- and 4-way bank conflicts (C3: 1.84 conflict cycles per LDS cycle).
+constexpr int kPkSph = 10;
+
 struct PacketScene {
-    const double* sph;   // LDS: cx cy cz r²
-    const double* rad;   // LDS: radius (culling only)
-    const double* pre;   // LDS: camera-ray oc.xyz, oc·oc − r²
-    const float* cone;   // LDS: camera-cone terms (cone_terms)
+    const double* sph;   // LDS: sphere records (kPkSph doubles, above)
     const double* pl;    // LDS: planes (px py pz nx ny nz (p−cam)·n −)
     const double* lt;    // LDS: point lights
     const double* tri;   // HBM
@@ -218,8 +224,9 @@ __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 axis, 
     const float ax = static_cast<float>(axis.x), ay = static_cast<float>(axis.y),
                 az = static_cast<float>(axis.z);
     auto test = [&](int k) {
-        const float4 a = reinterpret_cast<const float4*>(S.cone)[2 * k];
-        const float4 b = reinterpret_cast<const float4*>(S.cone)[2 * k + 1];
+        const float4* c4 = reinterpret_cast<const float4*>(S.sph + kPkSph * k + 4);
+        const float4 a = c4[0];
+        const float4 b = c4[1];
         const float q = a.w, rr = b.x, dv = b.y, slack = b.z;
         // θ + β ≥ π, or the axis is outside the cone around C−o (NaN q: always kept)
         return !(q > -cs * dv + slack) ||
@@ -260,10 +267,11 @@ __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, 
     const float inv_sl2 = 1.0f / sl2;  // wave-uniform; only read when sl2 > 0
     const float Rc = fmaxf(R, f32_up(RL)) + f32_up(fabs(bias)) * 1.001f;  // |n| ≤ 1 + 2ε
     auto test = [&](int k) {
-        const double* s = S.sph + kSphStride * k;
-        const float r = f32_up(S.rad[k]);
-        const float vx = static_cast<float>(s[0] - c.x), vy = static_cast<float>(s[1] - c.y),
-                    vz = static_cast<float>(s[2] - c.z);
+        const double2* s2 = reinterpret_cast<const double2*>(S.sph + kPkSph * k);
+        const double2 sxy = s2[0], szr = s2[1];  // cx cy | cz r² (two ds_read_b128)
+        const float r = reinterpret_cast<const float4*>(s2 + 2)[1].w;  // f32_up(radius)
+        const float vx = static_cast<float>(sxy.x - c.x), vy = static_cast<float>(sxy.y - c.y),
+                    vz = static_cast<float>(szr.x - c.z);
         const float vs = dot3f(vx, vy, vz, sx, sy, sz);
         const float vv = dot3f(vx, vy, vz, vx, vy, vz);
         float d2;
@@ -479,9 +487,9 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
             while (m) {
                 const int i = c * 64 + __builtin_ctzll(m);
                 m &= m - 1;
-                const double* q = S.pre + 4 * i;
-                const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
-                const double disc = b * b - four_a * q[3];
+                const double* q = S.sph + kPkSph * i;
+                const double b = 2.0 * dot(o - mk(q[0], q[1], q[2]), d);  // oc = cam − C
+                const double disc = b * b - four_a * q[8];
                 sphere_roots_core<(MAXC > 1)>(b, disc, two_a, r2a, i, S.orig, found, best, prim);
             }
         }
@@ -493,9 +501,9 @@ __device__ __forceinline__ bool closest_camera(const PacketScene& S, const Masks
             while (m) {
                 const int i = c * 64 + __builtin_ctzll(m);
                 m &= m - 1;
-                const double* q = S.pre + 4 * i;
-                const double b = 2.0 * dot(mk(q[0], q[1], q[2]), d);
-                const double disc = b * b - four_a * q[3];
+                const double* q = S.sph + kPkSph * i;
+                const double b = 2.0 * dot(o - mk(q[0], q[1], q[2]), d);  // oc = cam − C
+                const double disc = b * b - four_a * q[8];
                 if (regular) sphere_roots<(MAXC > 1)>(b, disc, two_a, i, S.orig, found, best, prim);
                 else sphere_roots_literal<(MAXC > 1)>(b, disc, two_a, i, S.orig, found, best, prim);
             }
@@ -530,7 +538,7 @@ __device__ __forceinline__ bool closest_masked(const PacketScene& S, const Masks
         while (m) {
             const int i = c * 64 + __builtin_ctzll(m);
             m &= m - 1;
-            const double* s = S.sph + kSphStride * i;
+            const double* s = S.sph + kPkSph * i;
             const d3 oc = o - mk(s[0], s[1], s[2]);
             const double b = 2.0 * dot(oc, d);
             const double cc = dot(oc, oc) - s[3];
@@ -561,7 +569,7 @@ __device__ __forceinline__ const double* pk_material(const PacketScene& S, const
 
 __device__ __forceinline__ d3 pk_normal(const PacketScene& S, const PkHit& h, d3 p) {
     if (h.prim < S.ns) {
-        const double* s = S.sph + kSphStride * h.prim;
+        const double* s = S.sph + kPkSph * h.prim;
         return unit(p - mk(s[0], s[1], s[2]));
     }
     if (h.prim < S.ns + S.np) {
@@ -627,7 +635,7 @@ __device__ __forceinline__ int pk_occlusion(const PacketScene& S, const Masks<MA
         while (m) {
             const int i = c * 64 + __builtin_ctzll(m);
             m &= m - 1;
-            const double* s = S.sph + kSphStride * i;
+            const double* s = S.sph + kPkSph * i;
             const d3 oc = o - mk(s[0], s[1], s[2]);
             const double b = 2.0 * dot(oc, d);
             const double cc = dot(oc, oc) - s[3];
@@ -846,8 +854,7 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
 __host__ __device__ inline int pk_chunk_bounds(int ns) { return ns >= kSphChunkMin ? (ns + 63) / 64 : 0; }
 __host__ __device__ inline size_t pk_image_bytes(int ns, int np, int nl) {
     const size_t nsb = static_cast<size_t>(ns) + pk_chunk_bounds(ns);
-    const size_t b = sizeof(double) * (static_cast<size_t>(kSphStride + 1 + 4) * nsb +
-                                       static_cast<size_t>(4) * ns +
+    const size_t b = sizeof(double) * (static_cast<size_t>(kPkSph) * nsb +
                                        static_cast<size_t>(kPlStride + 4) * np +
                                        static_cast<size_t>(kLtStride) * nl) +
                      (pk_chunk_bounds(ns) ? sizeof(int32_t) * ns : 0);
@@ -857,40 +864,39 @@ __host__ __device__ inline size_t pk_image_bytes(int ns, int np, int nl) {
 __device__ __forceinline__ void pk_build_image(const TraceParams& P, double* img, int tid,
                                                int nthreads) {
     const int ns = P.ns, np = P.np, nl = P.nl, nb = pk_chunk_bounds(ns), nsb = ns + nb;
-    double* s_sph = img;                                          // 32·nsb bytes
-    float* s_cone = reinterpret_cast<float*>(s_sph + kSphStride * nsb);  // 16-byte aligned
-    double* s_rad = s_sph + (kSphStride + 4) * nsb;
-    double* s_pre = s_rad + nsb;
-    double* s_pl = s_pre + 4 * ns;
+    double* s_sph = img;                                          // 80·nsb bytes
+    double* s_pl = s_sph + kPkSph * nsb;
     double* s_lt = s_pl + kPlStride * np;
     double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
     int32_t* s_orig = reinterpret_cast<int32_t*>(s_pln + 4 * np);  // nb > 0 only
     const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     const int32_t* perm = nb ? P.sph_perm : nullptr;
-    for (int i = tid; i < kSphStride * ns; i += nthreads)
-        s_sph[i] = P.sph[kSphStride * (perm ? perm[i / kSphStride] : i / kSphStride) + i % kSphStride];
     for (int i = tid; i < nb; i += nthreads) {  // chunk bounds as pseudo-spheres ns + c
         const double* q = P.sph_bnd + 4 * i;
-        double* o = s_sph + kSphStride * (ns + i);
+        double* o = s_sph + kPkSph * (ns + i);
         o[0] = q[0];
         o[1] = q[1];
         o[2] = q[2];
         o[3] = q[3] * q[3];
-        s_rad[ns + i] = q[3];
-        cone_terms(o, q[3], cam, s_cone + 8 * (ns + i));
+        o[8] = 0.0;
+        o[9] = 0.0;
+        cone_terms(o, q[3], cam, reinterpret_cast<float*>(o + 4));
     }
     for (int i = tid; i < ns; i += nthreads) {
         const int si = perm ? perm[i] : i;
         if (perm) s_orig[i] = si;
         const double* s = P.sph + kSphStride * si;
-        s_rad[i] = sqrt(s[3]);  // culling radius (only ever used with a margin)
-        cone_terms(s, s_rad[i], cam, s_cone + 8 * i);
-        // camera-ray constants of Sphere::Intersect (Shape.h:73,77)
+        double* o = s_sph + kPkSph * i;
+        o[0] = s[0];
+        o[1] = s[1];
+        o[2] = s[2];
+        o[3] = s[3];
+        o[9] = 0.0;
+        // culling radius (only ever used with a margin, rounded up to FP32 in cone_terms)
+        cone_terms(s, sqrt(s[3]), cam, reinterpret_cast<float*>(o + 4));
+        // camera-ray constant of Sphere::Intersect (Shape.h:73,77)
         const d3 oc = cam - mk(s[0], s[1], s[2]);
-        s_pre[4 * i + 0] = oc.x;
-        s_pre[4 * i + 1] = oc.y;
-        s_pre[4 * i + 2] = oc.z;
-        s_pre[4 * i + 3] = dot(oc, oc) - s[3];
+        o[8] = dot(oc, oc) - s[3];
     }
     for (int i = tid; i < np; i += nthreads) {
         const double* p = P.pl + kPlStride * i;
@@ -943,11 +949,8 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
         if (P.tile_cost) t_start = __builtin_amdgcn_s_memrealtime();
     const int ns = P.ns, np = kNoPL ? 0 : P.np, nl = kNoPL ? 0 : P.nl, nb = pk_chunk_bounds(ns),
               nsb = ns + nb;
-    double* s_sph = smem;                                         // 32·nsb bytes
-    float* s_cone = reinterpret_cast<float*>(s_sph + kSphStride * nsb);  // 16-byte aligned
-    double* s_rad = s_sph + (kSphStride + 4) * nsb;
-    double* s_pre = s_rad + nsb;
-    double* s_pl = s_pre + 4 * ns;
+    double* s_sph = smem;                                         // 80·nsb bytes
+    double* s_pl = s_sph + kPkSph * nsb;
     double* s_lt = s_pl + kPlStride * np;
     double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
     const int32_t* s_orig = reinterpret_cast<const int32_t*>(s_pln + 4 * np);
@@ -1004,9 +1007,6 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
 
     PacketScene S;
     S.sph = s_sph;
-    S.rad = s_rad;
-    S.cone = s_cone;
-    S.pre = s_pre;
     S.pl = s_pl;
     S.lt = s_lt;
     S.tri = P.tri;
@@ -1262,7 +1262,8 @@ void packet_grid(const TraceParams& p, uint32_t& gx, uint32_t& gy, uint32_t& wav
 constexpr int kOrderBins = 16;
 __global__ __launch_bounds__(1024) void packet_order_kernel(const uint32_t* cost, uint32_t gx,
                                                             uint32_t gy, uint32_t waves,
-                                                            uint32_t* keys, uint32_t* order) {
+                                                            uint32_t* keys, uint32_t* order,
+                                                            uint32_t* verdict) {
     __shared__ uint32_t s_max, s_cnt[kOrderBins];
     const uint32_t tid = threadIdx.x, tiles = gx * gy;
     if (tid == 0) s_max = 0;
@@ -1299,6 +1300,10 @@ __global__ __launch_bounds__(1024) void packet_order_kernel(const uint32_t* cost
         }
     }
     const bool narrow = median_bin >= kOrderBins / 4;
+    // for the host (pinned memory): 1 = narrow, launches keep the default order without even
+    // reading the table (its per-workgroup load cost C2 3 %); 2 = dispatch by the table
+    if (tid == 0 && verdict) __hip_atomic_store(verdict, narrow ? 1u : 2u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_SYSTEM);
     // one wave scatters the tiles in default dispatch order (bottom-up rows), stably per bin:
     // lane b < kOrderBins holds bin b's cursor
     uint32_t cur = 0;
@@ -1329,9 +1334,10 @@ __global__ __launch_bounds__(1024) void packet_order_kernel(const uint32_t* cost
 }
 
 hipError_t launch_packet_order(const uint32_t* cost, uint32_t gx, uint32_t gy, uint32_t waves,
-                               uint32_t* keys, uint32_t* order, hipStream_t stream) {
+                               uint32_t* keys, uint32_t* order, uint32_t* verdict,
+                               hipStream_t stream) {
     hipLaunchKernelGGL(packet_order_kernel, dim3(1), dim3(1024), 0, stream, cost, gx, gy, waves,
-                       keys, order);
+                       keys, order, verdict);
     return hipGetLastError();
 }
 #endif

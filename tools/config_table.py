@@ -65,8 +65,14 @@ for name in names:
         med = sorted(ms)[len(ms) // 2]
         row.update({"cpu_sample": f"same scene at {W // k}x{H // k}, 3 frames, median",
                     "cpu_threads": used, "cpu_ms_per_sample_frame": round(med, 2),
-                    "cpu_mrays_s": round(srays / med / 1e3, 2),
-                    "gpu_over_cpu": round(rays / best / (srays / med), 1)})
+                    "cpu_mrays_s": round(srays / med / 1e3, 2)})
+        ratio = round(rays / best / (srays / med), 1)
+        if name == "bigmesh":
+            # not a speed-up of the same algorithm: the GPU path traverses a triangle BVH, the
+            # reference tests every triangle of every model for every ray (Shape.h:263-307)
+            row["gpu_bvh_over_cpu_brute_force"] = ratio
+        else:
+            row["gpu_over_cpu"] = ratio
     rows.append(row)
     print(json.dumps(row), file=sys.stderr, flush=True)
 print(json.dumps(rows, indent=1))
