@@ -230,11 +230,13 @@ __device__ __forceinline__ double u01(uint64_t seed, uint64_t pixel, uint32_t st
     return u01_key(pixel_key(seed, pixel), stream, index);
 }
 
-// Sky colour, Scene::backgroundColor (Scene.h:30-33).
-__device__ __forceinline__ d3 sky(d3 dir) {
-    const double t = 0.5 * (unit(dir).y + 1.0);
+// Sky colour, Scene::backgroundColor (Scene.h:30-33), in two steps: its blend weight (the only
+// thing it needs of the direction) and the colour from it.
+__device__ __forceinline__ double sky_weight(d3 dir) { return 0.5 * (unit(dir).y + 1.0); }
+__device__ __forceinline__ d3 sky_color(double t) {
     return mk(1.0, 1.0, 1.0) * (1.0 - t) + mk(0.5, 0.7, 1.0) * t;
 }
+__device__ __forceinline__ d3 sky(d3 dir) { return sky_color(sky_weight(dir)); }
 
 // ------------------------------------------------------------------ tonemap operators
 // RaytracingEngine.cpp:70-174.  Float literals are float-rounded then promoted, and the

@@ -1182,11 +1182,18 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
         acc = acc + col;
         samples += 1;
     }
-    if (valid) {
+    // The pixel again, from the lane id (mbcnt) and the workgroup's tile (scalars): keeping x /
+    // yl live across the trace cost the single-sample variants a spilled dword per lane, whose
+    // scratch write-back was most of C2's HBM traffic beyond the framebuffer (12 MB per frame).
+    const uint32_t lane_e = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const uint32_t wave_e = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wave));
+    const uint32_t x_e = tbx * (kPkW * kWgWavesX) + (wave_e % kWgWavesX) * kPkW + (lane_e % kPkW);
+    const uint32_t yl_e = tby * (kPkH * WGY) + (wave_e / kWgWavesX) * kPkH + (lane_e / kPkW);
+    if (x_e < P.width && yl_e < P.rows) {
         // accumulated / samples (Scene.h:298-300); x / 1.0 == x, so AA=1 skips the division
         const d3 v = samples == 1 ? acc
                    : (samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0));
-        const size_t o = static_cast<size_t>(yl) * P.width + x;
+        const size_t o = static_cast<size_t>(yl_e) * P.width + x_e;
         if (P.out64) {
             P.out64[3 * o + 0] = v.x;
             P.out64[3 * o + 1] = v.y;
