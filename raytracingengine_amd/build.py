@@ -24,7 +24,7 @@ ARCH = "gfx950"
 HIP_FLAGS = ["-O3", "-std=c++20", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
              "-Wall", "-Wno-unused-result"]
 SOURCES = ["rt_trace.hip", "rt_trace_lean.hip", "rt_packet.hip", "rt_packet_area.hip",
-           "rt_wavefront.hip", "rt_wavefront_lean.hip", "rt_assemble.hip", "rt_capi.cpp",
+           "rt_wavefront.hip", "rt_wavefront_lean.hip", "rt_assemble.hip", "rt_box.hip", "rt_capi.cpp",
            "rt_multi.cpp", "rt_queue.cpp", "rt_bvh.cpp"]
 # RCCL (multi-GPU frames, rt_multi.cpp).  Inside a PyTorch process the loader reuses torch's
 # librccl.so.1 (same soname, loaded first by capi.load_library), so one RCCL serves both.

@@ -1,0 +1,361 @@
+// rt_box.hip — reflection chains of scenes made of planes only (no spheres, triangles or area
+// light): the reference main()'s own scene (RaytracingEngine.cpp:255-291, BASELINE config 1 — a
+// box of five axis-aligned mirrored walls lit by two point lights) and any box-like room.
+//
+// Same TraceRay chain as trace_chain (rt_trace_common.hpp: Scene.h:131-198 with transparency 0,
+// accumulated front to back), same shading helpers, so the image is bit-identical to the generic
+// chain kernel's.  What changes is how the planes are tested:
+//
+//  * The planes live in a per-scene table read through the scalar cache (wave-uniform loads into
+//    SGPRs), so no plane value occupies a VGPR or an LDS slot, grouped by the axis of their normal
+//    (x, y, z, then the rest) so the component a group needs is known at compile time.
+//  * A plane whose normal is exactly ±e_k (two zero components, the third ±1 — what the Plane
+//    constructor's normalize() makes of an axis direction, Shape.h:142) has, for a ray with finite
+//    origin o and direction d, num = (p − o)·n = s·(p_k − o_k) and denom = n·d = s·d_k exactly:
+//    the zero terms are signed zeros that cannot change a nonzero sum.  t = num/denom is then
+//    (p_k − o_k)/d_k bit for bit (IEEE division is sign-symmetric), i.e. one subtraction and a
+//    division through the shared reciprocal of d_k (div_core) instead of two dot products and a
+//    division.  p_k − o_k == 0 (a ray starting on the plane: t = ±0, the sign from the literal
+//    sum) and values outside div_core's range take the literal expression.
+//  * Shadow rays are classified (blocked / clear / undecided) from the same A = num·sign(denom),
+//    B = |denom| as the generic occlusion_opaque, which for such a plane are sign(d_k)·(p_k − o_k)
+//    and |d_k| exactly; undecided lanes run the exact computeTransmittance march.
+// Closest-hit ties between groups keep the reference's order: the lower scene index wins
+// (strict '<' in scene order, Shape.h:36 / Scene.h:233-241).
+#include "rt_trace_common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace rtamd {
+
+// Waves per SIMD the single-sample (AA = 1) and the multi-sample instantiations are compiled for.
+#ifndef RT_BOX_WAVES
+#define RT_BOX_WAVES 4
+#endif
+#ifndef RT_BOX_MULTI_WAVES
+#define RT_BOX_MULTI_WAVES 3
+#endif
+
+// wave-uniform reads through the scalar data cache
+typedef const __attribute__((address_space(4))) double* cdp;
+
+struct BoxScene {
+    cdp pl;           // box table, kBoxRec doubles per plane, in group order
+    const double* g;  // the same table for per-lane (vector) reads of the hit plane
+    cdp lt;           // point lights (kLtStride)
+    int n[4];         // planes per group: normal ±e_x, ±e_y, ±e_z, any other
+    int nl;
+};
+
+struct BoxHit {
+    double t;
+    int rec;   // the hit plane's record (group order)
+    int orig;  // its scene index
+};
+
+// |o_i| ≤ 2^1000 (with the table's |p_i| ≤ 2^1000 every p_i − o_i is finite, so the shortcut's
+// zero terms are signed zeros) and |d_i| ≤ 2^90 (finite; with 2^-900 ≤ |p_k − o_k| ≤ 2^900 and
+// |d_k| > 1e-6 every operand is in div_core's range, rt_device.hpp: |n/d| ≥ 2^-1000).  Camera and
+// reflection rays are unit vectors; NaN fails both.
+__device__ __forceinline__ bool box_ray_ok(d3 o, d3 d) {
+    return fabs(o.x) + fabs(o.y) + fabs(o.z) <= 0x1p1000 &&
+           fabs(d.x) + fabs(d.y) + fabs(d.z) <= 0x1p90;
+}
+
+__device__ __forceinline__ double comp(d3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+__device__ __forceinline__ int rec_orig(cdp q) { return __double2loint(q[15]); }
+
+// The reference's literal Plane::Intersect quotient (Shape.h:149-159); denom checked by the caller.
+__device__ __forceinline__ double plane_literal_t(cdp q, d3 o, d3 d) {
+    const d3 n = mk(q[3], q[4], q[5]);
+    return dot(mk(q[0], q[1], q[2]) - o, n) / dot(n, d);
+}
+
+// IntersectClosest's running minimum (Scene.h:233-241): strictly closer, or as close with a
+// lower scene index (the reference visits planes in scene order and keeps the first).
+__device__ __forceinline__ void box_take(double t, int rec, int orig, bool& found, BoxHit& h) {
+    if (t >= 0.0 && (!found || t < h.t || (t == h.t && orig < h.orig))) {
+        found = true;
+        h.t = t;
+        h.rec = rec;
+        h.orig = orig;
+    }
+}
+
+// Group K (normal ±e_K) of the closest-hit search, every lane's ray finite (box_ray_ok).
+template <int K>
+__device__ __forceinline__ void box_group_closest(const BoxScene& S, int first, d3 o, d3 d,
+                                                  bool& found, BoxHit& h) {
+    const int n = S.n[K];
+    if (n == 0) return;  // uniform
+    const double dk = comp(d, K), ok = comp(o, K);
+    const bool live = fabs(dk) > 1e-6;  // |denom| > 1e-6 (Shape.h:151)
+    const double rk = rcp_refined(dk);
+    for (int j = 0; j < n; ++j) {
+        cdp q = S.pl + kBoxRec * (first + j);
+        const double c = q[6] - ok;  // p_k − o_k
+        double t = div_core(c, dk, rk);
+        const bool odd = live && !(fabs(c) >= 0x1p-900 && fabs(c) <= 0x1p900);
+        if (__ballot(odd)) {  // uniform: some lane needs the literal quotient
+            if (odd) t = c == 0.0 ? plane_literal_t(q, o, d) : c / dk;
+        }
+        if (live) box_take(t, first + j, rec_orig(q), found, h);
+    }
+}
+
+// The reference's literal plane loop over records [first, first + n) (rays that are not finite,
+// and planes of no axis).
+__device__ __forceinline__ void box_literal_closest(const BoxScene& S, int first, int n, d3 o,
+                                                    d3 d, bool& found, BoxHit& h) {
+    for (int j = 0; j < n; ++j) {
+        cdp q = S.pl + kBoxRec * (first + j);
+        const d3 nn = mk(q[3], q[4], q[5]);
+        const double denom = dot(nn, d);
+        if (fabs(denom) > 1e-6) {
+            const double t = dot(mk(q[0], q[1], q[2]) - o, nn) / denom;
+            box_take(t, first + j, rec_orig(q), found, h);
+        }
+    }
+}
+
+// Scene::IntersectClosest over the planes (Scene.h:218-257; Plane::Intersect Shape.h:149-159).
+__device__ __forceinline__ bool box_closest(const BoxScene& S, d3 o, d3 d, BoxHit& h) {
+    bool found = false;
+    h.t = 0.0;
+    h.rec = 0;
+    h.orig = 0;
+    const int g1 = S.n[0], g2 = g1 + S.n[1], g3 = g2 + S.n[2];
+    if (__ballot(!box_ray_ok(o, d)) == 0) {  // uniform
+        box_group_closest<0>(S, 0, o, d, found, h);
+        box_group_closest<1>(S, g1, o, d, found, h);
+        box_group_closest<2>(S, g2, o, d, found, h);
+    } else {
+        box_literal_closest(S, 0, g3, o, d, found, h);
+    }
+    box_literal_closest(S, g3, S.n[3], o, d, found, h);
+    return found;
+}
+
+// Shadow-ray classification of one plane from A = num·sign(denom), B = |denom| (as
+// occlusion_opaque): t < 0, beyond the light, blocking, or undecided (near a threshold).
+__device__ __forceinline__ void box_classify(double A, double B, double max_dist, double bias,
+                                             bool& blocked, bool& undecided) {
+    if (A < -1e-300 * B) return;
+    if (A >= max_dist * B * (1.0 + 1e-9)) return;
+    if (A > bias * B * (1.0 + 1e-9) && A < max_dist * B * (1.0 - 1e-9)) blocked = true;
+    else undecided = true;
+}
+
+template <int K>
+__device__ __forceinline__ void box_group_occlusion(const BoxScene& S, int first, d3 o, d3 d,
+                                                    double max_dist, double bias, bool& blocked,
+                                                    bool& undecided) {
+    const int n = S.n[K];
+    if (n == 0) return;  // uniform
+    const double dk = comp(d, K), ok = comp(o, K);
+    const double B = fabs(dk);
+    if (!(B > 1e-6)) return;  // |denom| ≤ 1e-6: no plane of the group can be hit
+    for (int j = 0; j < n; ++j) {
+        cdp q = S.pl + kBoxRec * (first + j);
+        const double c = q[6] - ok;
+        box_classify(dk > 0.0 ? c : -c, B, max_dist, bias, blocked, undecided);
+    }
+}
+
+__device__ __forceinline__ void box_literal_occlusion(const BoxScene& S, int first, int n, d3 o,
+                                                      d3 d, double max_dist, double bias,
+                                                      bool& blocked, bool& undecided) {
+    for (int j = 0; j < n; ++j) {
+        cdp q = S.pl + kBoxRec * (first + j);
+        const d3 nn = mk(q[3], q[4], q[5]);
+        const double denom = dot(nn, d);
+        if (!(fabs(denom) > 1e-6)) continue;
+        const double num = dot(mk(q[0], q[1], q[2]) - o, nn);
+        box_classify(denom > 0.0 ? num : -num, fabs(denom), max_dist, bias, blocked, undecided);
+    }
+}
+
+// computeTransmittance (Scene.h:35-77) of an opaque planes-only scene: 1 clear, 0 blocked, -1
+// undecided (the exact march decides).
+__device__ __forceinline__ int box_occlusion(const BoxScene& S, d3 o, d3 d, double max_dist,
+                                             double bias) {
+    bool blocked = false, undecided = false;
+    const int g1 = S.n[0], g2 = g1 + S.n[1], g3 = g2 + S.n[2];
+    if (__ballot(!box_ray_ok(o, d)) == 0) {  // uniform
+        box_group_occlusion<0>(S, 0, o, d, max_dist, bias, blocked, undecided);
+        box_group_occlusion<1>(S, g1, o, d, max_dist, bias, blocked, undecided);
+        box_group_occlusion<2>(S, g2, o, d, max_dist, bias, blocked, undecided);
+    } else {
+        box_literal_occlusion(S, 0, g3, o, d, max_dist, bias, blocked, undecided);
+    }
+    box_literal_occlusion(S, g3, S.n[3], o, d, max_dist, bias, blocked, undecided);
+    return undecided ? -1 : (blocked ? 0 : 1);
+}
+
+// The exact march (transmittance(), rt_trace_common.hpp) over the planes.
+__device__ __forceinline__ double box_transmittance(const BoxScene& S, d3 o, d3 d,
+                                                    double max_dist, double bias) {
+    double T = 1.0, traveled = 0.0;
+    int safety = 64;
+    while (safety-- > 0 && T > 1e-4 && traveled < max_dist) {
+        BoxHit h;
+        if (!box_closest(S, o, d, h)) break;
+        const double t = h.t;
+        if (t <= 0.0) {
+            o = o + d * bias;
+            traveled += bias;
+            continue;
+        }
+        if (t <= bias) {
+            o = (o + d * t) + d * bias;
+            traveled += t + bias;
+            continue;
+        }
+        if (traveled + t >= max_dist) break;
+        T *= sclamp(S.g[kBoxRec * h.rec + 13], 0.0, 1.0);
+        o = (o + d * t) + d * bias;
+        traveled += t + bias;
+    }
+    return sclamp(T, 0.0, 1.0);
+}
+
+// One TraceRay level (shade<false>, rt_trace_common.hpp) for a planes-only opaque scene:
+// the local light of the hit (or the sky) and the reflection ray.
+template <bool COUNT>
+__device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& P, d3 o, d3 d,
+                                          Counts& cnt) {
+    Node nd;
+    nd.refl = false;
+    nd.refr = false;
+    if (COUNT) cnt.trace++;
+    BoxHit h;
+    if (!box_closest(S, o, d, h)) {
+        nd.hit = false;
+        nd.value = sky(d);
+        return nd;
+    }
+    nd.hit = true;
+    const double bias = P.bias;
+    const d3 hp = o + d * h.t;  // Rayon::pointAtDistance
+    const double* r = S.g + kBoxRec * h.rec;
+    const d3 gn = mk(r[3], r[4], r[5]);  // Plane::GetNormalAt (Shape.h:161-163)
+    const bool unit_n = r[7] != 0.0;     // |n| rounds to exactly 1: normalize() returns n
+    const Mat m = load_mat(r + 8);
+    const d3 inc = unit(d);
+    const bool front = dot(gn, inc) < 0.0;
+    const d3 n0 = front ? gn : -gn;
+    const d3 view = -inc;
+    const double tr = sclamp(m.transparency, 0.0, 1.0);
+    // directLightning (Scene.h:79-129)
+    const d3 n = unit_n ? n0 : unit(n0);
+    d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
+    for (int i = 0; i < S.nl; ++i) {
+        cdp l = S.lt + kLtStride * i;
+        const d3 lpos = mk(l[0], l[1], l[2]), E = mk(l[3], l[4], l[5]);
+        double dist, inv_d2;
+        d3 L;
+        light_dir(lpos - hp, dist, L, inv_d2);
+        if (dist <= 0.0) continue;
+        const double ndl = smax(0.0, dot(n, L));
+        if (ndl <= 0.0) continue;
+        if (dist <= bias) continue;
+        if (COUNT) cnt.shadow++;
+        const d3 so = hp + n * bias;
+        const int occ = box_occlusion(S, so, L, dist - bias, bias);
+        const double T = occ >= 0 ? static_cast<double>(occ)
+                                  : box_transmittance(S, so, L, dist - bias, bias);
+        if (T <= bias) continue;
+        diff = diff + ((E * inv_d2) * ndl) * T;
+        if (m.transparency <= 0.0 && m.specular > 0.0) {
+            const d3 H = unit(L + view);
+            const double ndh = smax(0.0, dot(n, H));
+            if (ndh > 0.0) {
+                const double sf = pow_bp_t<true>(ndh, m.shininess);
+                spec = spec + ((E * inv_d2) * sf) * T;
+            }
+        }
+    }
+    const d3 local = hmul(m.color, diff) + spec * m.specular;
+    d3 fin = mk(0.0, 0.0, 0.0);
+    if (tr < 1.0) fin = fin + local * (1.0 - tr);
+    nd.value = fin;
+    if (m.specular > bias) {
+        const d3 R = unit(reflect(inc, n0));
+        nd.refl = true;
+        nd.rd = R;
+        nd.ro = hp + R * bias;
+        nd.rw = m.specular;
+    }
+    return nd;
+}
+
+// GeneratePixelAt (Scene.h:283-304) → TraceRay as a reflection chain accumulated front to back
+// (trace_chain's order, so the image equals the generic chain kernel's bit for bit).
+template <bool COUNT, bool SINGLE>
+__global__ __launch_bounds__(kTileW * kTileH, SINGLE ? RT_BOX_WAVES : RT_BOX_MULTI_WAVES) void box_chain_kernel(TraceParams P) {
+    const uint32_t x = blockIdx.x * kTileW + threadIdx.x;
+    const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
+    Counts cnt{0u, 0u};
+    BoxScene S;
+    S.pl = (cdp)P.box;
+    S.g = P.box;
+    S.lt = (cdp)P.lt;
+    for (int k = 0; k < 4; ++k) S.n[k] = P.box_n[k];
+    S.nl = P.nl;
+    if (x < P.width && yl < P.rows) {
+        const uint32_t y = image_row(P, yl);
+        const uint64_t pix = static_cast<uint64_t>(y) * P.width + x;
+        const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+        d3 acc = mk(0.0, 0.0, 0.0);
+        int samples = 0;
+        const int nsamples = SINGLE ? 1 : P.aa;
+        for (int s = 0; s < nsamples; ++s) {
+            d3 d = camera_dir(P, cam, x, y, pix, s);
+            d3 o = cam;
+            d3 c = mk(0.0, 0.0, 0.0);
+            double w = 1.0;
+            for (int depth = 0;; ++depth) {
+                if (depth >= P.max_rec) {  // TraceRay at depth maxRecursion: the sky
+                    c = c + sky(d) * w;
+                    break;
+                }
+                const Node nd = box_shade<COUNT>(S, P, o, d, cnt);
+                c = c + nd.value * w;
+                if (!nd.hit || !nd.refl) break;
+                w = w * nd.rw;
+                o = nd.ro;
+                d = nd.rd;
+            }
+            acc = acc + c;
+            samples += 1;
+        }
+        const d3 v = samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0);
+        store_pixel(P, static_cast<size_t>(yl) * P.width + x, v);
+    }
+    if constexpr (COUNT) {
+        uint32_t t = cnt.trace, s = cnt.shadow;
+        for (int off = 32; off > 0; off >>= 1) {
+            t += __shfl_xor(t, off, 64);
+            s += __shfl_xor(s, off, 64);
+        }
+        if (((threadIdx.y * kTileW + threadIdx.x) & 63) == 0) {
+            atomicAdd(P.counters + 0, static_cast<unsigned long long>(t));
+            atomicAdd(P.counters + 1, static_cast<unsigned long long>(s));
+        }
+    }
+}
+
+hipError_t launch_box_chain(const TraceParams& p, bool count, hipStream_t stream) {
+    const dim3 block(kTileW, kTileH);
+    const dim3 grid((p.width + kTileW - 1) / kTileW, (p.rows + kTileH - 1) / kTileH);
+    if (count) {
+        if (p.aa == 1) hipLaunchKernelGGL((box_chain_kernel<true, true>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((box_chain_kernel<true, false>), grid, block, 0, stream, p);
+    } else {
+        if (p.aa == 1) hipLaunchKernelGGL((box_chain_kernel<false, true>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((box_chain_kernel<false, false>), grid, block, 0, stream, p);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace rtamd

@@ -147,6 +147,10 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
         p.bvh_tri = reinterpret_cast<const int32_t*>(base + sc->off_bvh_tri);
     }
     p.lt = base + sc->off_lt;
+    if (sc->np > 0) {
+        p.box = base + sc->off_box;
+        for (int k = 0; k < 4; ++k) p.box_n[k] = sc->box_n[k];
+    }
     if (sc->ns >= kSphChunkMin) {
         p.sph_bnd = base + sc->off_sbnd;
         p.sph_perm = reinterpret_cast<const int32_t*>(base + sc->off_sperm);
@@ -402,7 +406,11 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
     }
     // generic kernels without triangle / area-light code for scenes that use neither
     const bool lean_generic = p.nt == 0 && p.al_samples == 0;
+    // reflection chains of scenes made of planes only take the planes-only chain kernel
+    const bool box = path == kPathChain && p.ns == 0 && p.nt == 0 && p.al_samples == 0 &&
+                     p.np > 0 && !(flags & RT_FLAG_GENERIC_KERNEL);
     auto launch = [&](const TraceParams& q, bool count) {
+        if (box) return launch_box_chain(q, count, ctx->stream);
         return packet ? launch_packet_direct(q, count, sc->max_specular > 0.0, ctx->stream)
                       : (lean_generic ? lean::launch_trace(q, path, count, lds, lds_bytes, ctx->stream)
                                       : launch_trace(q, path, count, lds, lds_bytes, ctx->stream));
@@ -656,6 +664,44 @@ rt_status rt_scene_create(rt_context* ctx, const rt_scene_desc* d, rt_scene** ou
         h.resize(sc->off_sperm + (perm.size() + 1) / 2 + 2, 0.0);
         std::memcpy(&h[sc->off_sbnd], bnd.data(), bnd.size() * sizeof(double));
         std::memcpy(&h[sc->off_sperm], perm.data(), perm.size() * sizeof(int32_t));
+    }
+
+    // planes-only chain table (rt_box.hip): the planes grouped by the axis of their normal —
+    // exactly ±e_x, ±e_y, ±e_z (two zero components, the third ±1), then the rest — each group
+    // in scene order, with the plane's material, a flag for normals whose normalize() returns
+    // them unchanged (|n| rounds to 1: sqrt of the reference's dot, correctly rounded as on the
+    // device) and the scene index for closest-hit ties
+    if (sc->np > 0) {
+        std::vector<int> grp(sc->np);
+        for (int i = 0; i < sc->np; ++i) {
+            const double* q = &h[sc->off_pl + size_t(kPlStride) * i];
+            const double* n = q + 3;
+            grp[i] = 3;
+            const bool bounded = std::fabs(q[0]) <= 0x1p1000 && std::fabs(q[1]) <= 0x1p1000 &&
+                                 std::fabs(q[2]) <= 0x1p1000;  // p − o stays finite (rt_box.hip)
+            for (int k = 0; k < 3 && bounded; ++k)
+                if (std::fabs(n[k]) == 1.0 && n[(k + 1) % 3] == 0.0 && n[(k + 2) % 3] == 0.0)
+                    grp[i] = k;
+        }
+        sc->off_box = (h.size() + 1) & ~size_t(1);
+        h.resize(sc->off_box + size_t(kBoxRec) * sc->np + 2, 0.0);
+        size_t r = 0;
+        for (int g = 0; g < 4; ++g) {
+            for (int i = 0; i < sc->np; ++i) {
+                if (grp[i] != g) continue;
+                const double* pl = &h[sc->off_pl + size_t(kPlStride) * i];
+                double* o = &h[sc->off_box + size_t(kBoxRec) * r++];
+                for (int k = 0; k < 6; ++k) o[k] = pl[k];
+                o[6] = g < 3 ? pl[g] : 0.0;
+                const double nn = pl[3] * pl[3] + pl[4] * pl[4] + pl[5] * pl[5];
+                o[7] = std::sqrt(nn) == 1.0 ? 1.0 : 0.0;
+                for (int k = 0; k < kMatStride - 1; ++k)
+                    o[8 + k] = h[sc->off_pl_mat + size_t(kMatStride) * i + k];
+                const int32_t idx[2] = {i, 0};
+                std::memcpy(&o[15], idx, sizeof idx);
+                ++sc->box_n[g];
+            }
+        }
     }
 
     hipError_t e = sc->buf.ensure(h.size() * sizeof(double));

@@ -92,6 +92,8 @@ struct rt_scene {
     size_t off_bvh = 0, off_bvh_tri = 0;  // triangle BVH, when bvh_nodes > 0
     int32_t bvh_nodes = 0;
     size_t off_sperm = 0, off_sbnd = 0;   // sphere chunks, when ns >= kSphChunkMin
+    size_t off_box = 0;                   // planes-only chain table (rt_box.hip), when np > 0
+    int32_t box_n[4] = {0, 0, 0, 0};
     // Packet-kernel LDS images, one per camera position this scene was rendered from more than
     // once (the image depends on the spheres, planes, point lights and camera position only).  An
     // entry is written once, by packet_image_kernel on the stream of the render that created

@@ -145,7 +145,26 @@ __device__ __forceinline__ void light_dir(d3 v, double& dist, d3& L, double& inv
 // tests hold libm-pow scenes to.  Inputs outside x ∈ (0, 1.5), |y| ≤ 2^60 (none in a trace: N·H
 // is in (0, 1 + 4ε]) call the libm pow out of line.
 __device__ __noinline__ double pow_libm(double x, double y) { return pow(x, y); }
-__device__ __forceinline__ double pow_bp(double x, double y) {
+
+// An FP64 constant materialized into an SGPR pair at its point of use (two s_mov_b32 that the
+// compiler may not hoist).  gfx950 VALU instructions take no 64-bit literal, so the compiler
+// keeps every FP64 constant of a loop body in registers for the whole loop; in a reflection
+// chain that is pow_bp's 26 polynomial constants, 36 VGPRs held across every level (rt_box.hip:
+// 167 -> 131 VGPRs).  Same value, same bits: only where it is formed changes.
+template <uint64_t B>
+__device__ __forceinline__ double kc_bits() {
+    uint32_t lo, hi;
+    asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3"
+                 : "=s"(lo), "=s"(hi)
+                 : "i"(static_cast<uint32_t>(B)), "i"(static_cast<uint32_t>(B >> 32)));
+    return __hiloint2double(static_cast<int>(hi), static_cast<int>(lo));
+}
+#define RT_KC(x) ::rtamd::kc_bits<__builtin_bit_cast(uint64_t, static_cast<double>(x))>()
+
+// KC: form the polynomial constants at their use (kc_bits) instead of as hoistable literals.
+template <bool KC = false>
+__device__ __forceinline__ double pow_bp_t(double x, double y) {
+#define RT_PC(v) (KC ? RT_KC(v) : static_cast<double>(v))
     if (!(x > 0.0 && x < 1.5 && fabs(y) <= 0x1p60)) return pow_libm(x, y);
     int e;
     double m = frexp(x, &e);
@@ -155,43 +174,45 @@ __device__ __forceinline__ double pow_bp(double x, double y) {
     }
     const double s = (m - 1.0) / (m + 1.0);
     const double s2 = s * s;
-    double p = 1.0 / 23.0;
-    p = fma(p, s2, 1.0 / 21.0);
-    p = fma(p, s2, 1.0 / 19.0);
-    p = fma(p, s2, 1.0 / 17.0);
-    p = fma(p, s2, 1.0 / 15.0);
-    p = fma(p, s2, 1.0 / 13.0);
-    p = fma(p, s2, 1.0 / 11.0);
-    p = fma(p, s2, 1.0 / 9.0);
-    p = fma(p, s2, 1.0 / 7.0);
-    p = fma(p, s2, 1.0 / 5.0);
-    p = fma(p, s2, 1.0 / 3.0);
+    double p = RT_PC(1.0 / 23.0);
+    p = fma(p, s2, RT_PC(1.0 / 21.0));
+    p = fma(p, s2, RT_PC(1.0 / 19.0));
+    p = fma(p, s2, RT_PC(1.0 / 17.0));
+    p = fma(p, s2, RT_PC(1.0 / 15.0));
+    p = fma(p, s2, RT_PC(1.0 / 13.0));
+    p = fma(p, s2, RT_PC(1.0 / 11.0));
+    p = fma(p, s2, RT_PC(1.0 / 9.0));
+    p = fma(p, s2, RT_PC(1.0 / 7.0));
+    p = fma(p, s2, RT_PC(1.0 / 5.0));
+    p = fma(p, s2, RT_PC(1.0 / 3.0));
     const double ln_m = fma(2.0 * (s * s2), p, 2.0 * s);
     const double ed = static_cast<double>(e);
     constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
-    const double ln_x = fma(ed, kLn2Hi, fma(ed, kLn2Lo, ln_m));
+    const double ln_x = fma(ed, RT_PC(kLn2Hi), fma(ed, RT_PC(kLn2Lo), ln_m));
     const double z = y * ln_x;
     if (z < -1500.0) return 0.0;  // e^z below the subnormal range (and k fits an int below)
     if (z > 1500.0) return INFINITY;
-    const double kd = rint(z * 0x1.71547652b82fep0);
-    double r = fma(-kd, kLn2Hi, z);
-    r = fma(-kd, kLn2Lo, r);
-    double q = 1.0 / 6227020800.0;
-    q = fma(q, r, 1.0 / 479001600.0);
-    q = fma(q, r, 1.0 / 39916800.0);
-    q = fma(q, r, 1.0 / 3628800.0);
-    q = fma(q, r, 1.0 / 362880.0);
-    q = fma(q, r, 1.0 / 40320.0);
-    q = fma(q, r, 1.0 / 5040.0);
-    q = fma(q, r, 1.0 / 720.0);
-    q = fma(q, r, 1.0 / 120.0);
-    q = fma(q, r, 1.0 / 24.0);
-    q = fma(q, r, 1.0 / 6.0);
+    const double kd = rint(z * RT_PC(0x1.71547652b82fep0));
+    double r = fma(-kd, RT_PC(kLn2Hi), z);
+    r = fma(-kd, RT_PC(kLn2Lo), r);
+    double q = RT_PC(1.0 / 6227020800.0);
+    q = fma(q, r, RT_PC(1.0 / 479001600.0));
+    q = fma(q, r, RT_PC(1.0 / 39916800.0));
+    q = fma(q, r, RT_PC(1.0 / 3628800.0));
+    q = fma(q, r, RT_PC(1.0 / 362880.0));
+    q = fma(q, r, RT_PC(1.0 / 40320.0));
+    q = fma(q, r, RT_PC(1.0 / 5040.0));
+    q = fma(q, r, RT_PC(1.0 / 720.0));
+    q = fma(q, r, RT_PC(1.0 / 120.0));
+    q = fma(q, r, RT_PC(1.0 / 24.0));
+    q = fma(q, r, RT_PC(1.0 / 6.0));
     q = fma(q, r, 0.5);
     q = fma(q, r, 1.0);
     q = fma(q, r, 1.0);
     return ldexp(q, static_cast<int>(kd));
+#undef RT_PC
 }
+__device__ __forceinline__ double pow_bp(double x, double y) { return pow_bp_t<false>(x, y); }
 
 // std::max / std::min / std::clamp with libstdc++'s comparison order (NaN handling).
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }

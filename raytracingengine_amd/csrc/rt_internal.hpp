@@ -17,6 +17,10 @@ constexpr int kTriStride = 12;  // a0(3) e1(3) e2(3) n(3) (translated v0 and edg
                                 //                         untranslated normal, Shape.h:222-227)
 constexpr int kLtStride = 8;    // px py pz Ex Ey Ez - -  (E = color*intensity, Scene.h:110)
 constexpr int kMatStride = 8;   // r g b shininess specular transparency ior -
+// Planes-only chain kernel (rt_box.hip): one record per plane, in axis-group order —
+// p xyz | n xyz | p[k] (k = the group's axis) | 1 when |n| rounds to exactly 1 |
+// material (kMatStride - 1 doubles: r g b shininess specular transparency ior) | scene index (int)
+constexpr int kBoxRec = 16;
 
 constexpr int kBvhNodeStride = 8;  // triangle BVH node: lo xyz, hi xyz, {first, count}
 constexpr int kBvhMinTris = 32;    // scenes with fewer triangles test them all (no BVH)
@@ -88,6 +92,10 @@ struct TraceParams {
     // wave records its duration (per tile and wave) for the next order
     const uint32_t* tile_order;
     uint32_t* tile_cost;
+    // planes-only chain kernel: the box table (kBoxRec doubles per plane) and its group sizes —
+    // normal ±e_x, ±e_y, ±e_z, any other
+    const double* box;
+    int32_t box_n[4];
 };
 
 // Host: the spatial sphere chunks of the packet kernel's culls (rt_bvh.cpp): perm[sorted] =
@@ -112,6 +120,7 @@ namespace lean {  // rt_trace_lean.hip: the same kernels for scenes without tria
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
                         hipStream_t stream);
 }
+hipError_t launch_box_chain(const TraceParams& p, bool count, hipStream_t stream);
 hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specular,
                                 hipStream_t stream);
 size_t packet_lds_bytes(int ns, int np, int nl);

@@ -854,3 +854,67 @@ def _default_order(tiles, w):
     gy = tiles // gx
     lin = np.arange(tiles)
     return (gy - 1 - lin // gx) * gx + lin % gx
+
+
+# ------------------------------------------------------------------ planes-only chain kernel
+def _room_scene(kind):
+    """Planes-only reflection-chain scenes for the planes-only chain kernel (rt_box.hip)."""
+    mir = dict(specular=0.3, shininess=16.0)
+    if kind == "c1":          # the reference main()'s box at a reduced size
+        return make_config("c1", 120, 100)
+    if kind == "room":        # axis walls with signed-zero normals, one tilted wall, a plane far
+        sc = _scene(72, 56)   # away and two coincident walls of different colour (ties)
+        sc.add_plane((0, -3, 0), (0.0, 1.0, 0.0), Material((0.8, 0.8, 0.8), **mir))
+        sc.add_plane((0, 0, 10), (-0.0, -0.0, -1.0), Material((0.7, 0.8, 0.9), **mir))
+        sc.add_plane((4, 0, 0), (-1.0, 0.0, -0.0), Material((0.9, 0.3, 0.3), specular=0.5))
+        sc.add_plane((4, 0, 0), (-1.0, 0.0, 0.0), Material((0.1, 0.9, 0.3), specular=0.5))
+        sc.add_plane((-4, 0, 0), (1.0, 0.0, 0.0), Material((0.3, 0.3, 0.9), **mir))
+        sc.add_plane((3e303, 5.0, 0), (0.0, -1.0, 0.0), Material((0.5, 0.5, 0.5), **mir))
+        sc.add_plane((0, 6, 0), (0.3, -1.0, 0.2), Material((0.4, 0.4, 0.8), **mir))
+        sc.add_light((0, 2.5, -2), (1, 1, 1), 40)
+        sc.add_light((-2, -2.5, 8), (1, 0.5, 0.2), 25)
+        return sc
+    if kind == "on_floor":    # the camera exactly on the floor plane (camera rays start on it)
+        sc = SceneData(Camera((0.0, -3.0, -25.0), 32.0, 64, 48, 0.0, 200.0, 1))
+        sc.add_plane((0, -3, 0), (0.0, 1.0, 0.0), Material((0.8, 0.8, 0.8), **mir))
+        sc.add_plane((0, 0, 12), (0.0, 0.0, -1.0), Material((0.6, 0.7, 0.8), **mir))
+        sc.add_plane((0, 9, 0), (0.0, -1.0, 0.0), Material((0.9, 0.9, 0.5), **mir))
+        sc.add_light((1, 4, -3), (1, 1, 1), 60)
+        return sc
+    if kind == "huge":        # coordinates beyond the shortcut's bounds: the literal path
+        sc = SceneData(Camera((2.0 ** 1001, 0.0, -25.0), 32.0, 48, 32, 0.0, 200.0, 1))
+        sc.add_plane((0, -3, 0), (0.0, 1.0, 0.0), Material((0.8, 0.8, 0.8), **mir))
+        sc.add_plane((2.0 ** 1002, 0, 0), (-1.0, 0.0, 0.0), Material((0.9, 0.3, 0.3), **mir))
+        sc.add_light((0, 2.5, -2), (1, 1, 1), 40)
+        return sc
+    raise KeyError(kind)
+
+
+@pytest.mark.parametrize("kind", ["c1", "room", "on_floor", "huge"])
+@pytest.mark.parametrize("aa,max_rec", [(1, 10), (1, 1), (1, 16), (3, 4)])
+def test_box_chain_equals_generic_chain(ctx, kind, aa, max_rec):
+    """rt_box.hip (planes in axis groups read through the scalar cache, t = (p_k − o_k)/d_k,
+    shadow classification from the same A, B) renders every pixel bit-identical to the generic
+    chain kernel (RT_FLAG_GENERIC_KERNEL), with the same ray counts — including coincident
+    walls (closest-hit ties: lowest scene index), camera rays starting on a plane (t = ±0),
+    a tilted plane and coordinates outside the shortcut's bounds."""
+    sc = _room_scene(kind)
+    if aa != 1:
+        sc = sc.resized(sc.camera.width, sc.camera.height, aa)
+    out = _render(ctx, sc, hdr64=True, tonemap=6, stats=True,
+                  max_recursion=max_rec)
+    ref = _render(ctx, sc, hdr64=True, tonemap=6, stats=True,
+                  max_recursion=max_rec, flags=capi.RT_FLAG_GENERIC_KERNEL)
+    assert np.array_equal(out["hdr64"], ref["hdr64"], equal_nan=True)
+    assert np.array_equal(out["ldr"], ref["ldr"])
+    assert (out["trace_rays"], out["shadow_rays"]) == (ref["trace_rays"], ref["shadow_rays"])
+
+
+@pytest.mark.parametrize("kind", ["room", "on_floor"])
+def test_box_chain_vs_oracle(ctx, oracle, kind):
+    """The planes-only chain kernel against the C restatement (chains: ≤ 1e-12, Blinn-Phong pow)."""
+    sc = _room_scene(kind)
+    out = _render(ctx, sc, hdr64=True, stats=True)
+    ref, nt, ns = oracle.render(sc)
+    assert np.max(np.abs(out["hdr64"] - ref)) <= POW_TOL
+    assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)
