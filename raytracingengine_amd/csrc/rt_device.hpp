@@ -212,7 +212,7 @@ __device__ __forceinline__ double pow_bp_t(double x, double y) {
     return ldexp(q, static_cast<int>(kd));
 #undef RT_PC
 }
-__device__ __forceinline__ double pow_bp(double x, double y) { return pow_bp_t<false>(x, y); }
+__device__ __forceinline__ double pow_bp(double x, double y) { return pow_bp_t<true>(x, y); }
 
 // std::max / std::min / std::clamp with libstdc++'s comparison order (NaN handling).
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
