@@ -330,4 +330,23 @@ __device__ __forceinline__ void to_color(d3 v, uint8_t& r, uint8_t& g, uint8_t& 
     b = static_cast<uint8_t>(c.z * 255.0);
 }
 
+// toColor(reinhardSimple(c)) for one component (RaytracingEngine.cpp:70-72, 113-121): the byte
+// is trunc(fl(fl(c / (c + 1)) · 255)) after the clamp to [0, 1].  For 0 ≤ c ≤ 2^20 an FP32
+// estimate f of 255·c/(c+1) — conversion, add, v_rcp_f32 (1 ulp), two products: relative error
+// ≤ 6·2^-24 + 2^-23 < 5e-7, so |f − 255·c/(c+1)| < 1.3e-4 — decides the truncation whenever its
+// fraction is more than 5e-4 from an integer: the exact value (and the reference's FP64 result,
+// within 1e-13 of it) then has the same integer part.  Otherwise, and for c outside that range
+// (negative, NaN, huge), the reference's FP64 expression.
+__device__ __forceinline__ uint8_t reinhard_byte(double c) {
+    if (c >= 0.0 && c <= 0x1p20) {
+        const float cf = static_cast<float>(c);
+        const float f = (255.0f * cf) * __builtin_amdgcn_rcpf(cf + 1.0f);
+        const float fl = __builtin_floorf(f);
+        const float fr = f - fl;  // exact (f < 256)
+        if (fr > 5e-4f && fr < 1.0f - 5e-4f) return static_cast<uint8_t>(static_cast<int>(fl));
+    }
+    const double y = c / (c + 1.0);
+    return static_cast<uint8_t>(smin(1.0, smax(0.0, y)) * 255.0);
+}
+
 }  // namespace rtamd

@@ -1206,8 +1206,15 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
         }
         if (P.ldr) {
             uint8_t r, g, b;
-            if constexpr ((FEAT & kFeatJodie) != 0) to_color(tonemap_op(v, P.tonemap), r, g, b);
-            else to_color(tonemap_op_nolog(v, P.tonemap), r, g, b);
+            if (P.tonemap == 1) {  // uniform: Reinhard, through the FP32 byte decision
+                r = reinhard_byte(v.x);
+                g = reinhard_byte(v.y);
+                b = reinhard_byte(v.z);
+            } else if constexpr ((FEAT & kFeatJodie) != 0) {
+                to_color(tonemap_op(v, P.tonemap), r, g, b);
+            } else {
+                to_color(tonemap_op_nolog(v, P.tonemap), r, g, b);
+            }
             P.ldr[3 * o + 0] = r;
             P.ldr[3 * o + 1] = g;
             P.ldr[3 * o + 2] = b;
