@@ -167,6 +167,9 @@ typedef struct rt_render_opts {
                                       frame slots); rt_comm_synchronize waits for the frame   */
 #define RT_FLAG_NO_TILE_ORDER 0x20 /* ablation: the packet kernel's default tile order instead
                                       of costliest tiles first (the image is the same)        */
+#define RT_FLAG_NO_SAMPLE_PARALLEL 0x40 /* ablation: multi-sample planes-only chains loop over
+                                      the samples per thread instead of one thread per sample
+                                      (the image is the same)                                 */
 
 /* Fills opts with the reference defaults: max_recursion 10, bias 1e-3, tonemap ACES,
  * full image, seed 0x5EED, no flags. */

@@ -31,6 +31,7 @@ RT_FLAG_GENERIC_KERNEL = 0x4
 RT_FLAG_NO_BVH = 0x8
 RT_FLAG_PIPELINE = 0x10
 RT_FLAG_NO_TILE_ORDER = 0x20
+RT_FLAG_NO_SAMPLE_PARALLEL = 0x40
 RT_OUT_HDR64, RT_OUT_HDR32, RT_OUT_LDR = 0x1, 0x2, 0x4
 RT_COMM_ID_BYTES = 128
 

@@ -289,19 +289,104 @@ __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& 
     return nd;
 }
 
-// GeneratePixelAt (Scene.h:283-304) → TraceRay as a reflection chain accumulated front to back
-// (trace_chain's order, so the image equals the generic chain kernel's bit for bit).
-template <bool COUNT, bool SINGLE>
-__global__ __launch_bounds__(kTileW * kTileH, SINGLE ? RT_BOX_WAVES : RT_BOX_MULTI_WAVES) void box_chain_kernel(TraceParams P) {
-    const uint32_t x = blockIdx.x * kTileW + threadIdx.x;
-    const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
-    Counts cnt{0u, 0u};
+// One sample of GeneratePixelAt (Scene.h:283-304): TraceRay as a reflection chain accumulated
+// front to back (trace_chain's order, so the image equals the generic chain kernel's bit for bit).
+template <bool COUNT>
+__device__ __forceinline__ d3 box_sample(const BoxScene& S, const TraceParams& P, d3 cam,
+                                         uint32_t x, uint32_t y, uint64_t pix, int s, Counts& cnt) {
+    d3 d = camera_dir(P, cam, x, y, pix, s);
+    d3 o = cam;
+    d3 c = mk(0.0, 0.0, 0.0);
+    double w = 1.0;
+    for (int depth = 0;; ++depth) {
+        if (depth >= P.max_rec) {  // TraceRay at depth maxRecursion: the sky
+            c = c + sky(d) * w;
+            break;
+        }
+        const Node nd = box_shade<COUNT>(S, P, o, d, cnt);
+        c = c + nd.value * w;
+        if (!nd.hit || !nd.refl) break;
+        w = w * nd.rw;
+        o = nd.ro;
+        d = nd.rd;
+    }
+    return c;
+}
+
+__device__ __forceinline__ BoxScene box_scene(const TraceParams& P) {
     BoxScene S;
     S.pl = (cdp)P.box;
     S.g = P.box;
     S.lt = (cdp)P.lt;
     for (int k = 0; k < 4; ++k) S.n[k] = P.box_n[k];
     S.nl = P.nl;
+    return S;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void box_count(const Counts& cnt, const TraceParams& P, int tid) {
+    uint32_t t = cnt.trace, s = cnt.shadow;
+    for (int off = 32; off > 0; off >>= 1) {
+        t += __shfl_xor(t, off, 64);
+        s += __shfl_xor(s, off, 64);
+    }
+    if ((tid & 63) == 0) {
+        atomicAdd(P.counters + 0, static_cast<unsigned long long>(t));
+        atomicAdd(P.counters + 1, static_cast<unsigned long long>(s));
+    }
+}
+
+// Multi-sample frames, sample-parallel: thread t of a 256-thread workgroup traces sample
+// t mod aa of pixel t div aa (256 / aa consecutive pixels of the row-major frame per workgroup),
+// so every thread runs the single-sample code at the single-sample register budget (4
+// waves/SIMD, where a per-thread sample loop needs 3) and a wave's rays are the jittered
+// samples of one or a few pixels — more coherent than an 8×8 pixel tile.  The colours meet in
+// LDS, and one thread per pixel sums them in sample order (acc = acc + c, Scene.h:292-297) and
+// divides by the sample count: the same operations in the same order as the per-thread loop.
+constexpr int kBoxAaThreads = 256;
+constexpr int kBoxAaMax = 128;  // larger sample counts keep the per-thread loop
+template <bool COUNT>
+__global__ __launch_bounds__(kBoxAaThreads, RT_BOX_WAVES) void box_aa_kernel(TraceParams P) {
+    __shared__ double s_c[3 * kBoxAaThreads];
+    const int tid = threadIdx.x;
+    const int aa = P.aa;                     // 2 ≤ aa ≤ kBoxAaMax (launcher)
+    const int ppw = kBoxAaThreads / aa;      // pixels per workgroup
+    const int pl = tid / aa, s = tid - pl * aa;
+    const uint64_t npx = static_cast<uint64_t>(P.width) * P.rows;
+    const uint64_t lin = static_cast<uint64_t>(blockIdx.x) * ppw + pl;
+    Counts cnt{0u, 0u};
+    const BoxScene S = box_scene(P);
+    if (pl < ppw && lin < npx) {
+        const uint32_t x = static_cast<uint32_t>(lin % P.width);
+        const uint32_t y = image_row(P, static_cast<uint32_t>(lin / P.width));
+        const uint64_t pix = static_cast<uint64_t>(y) * P.width + x;
+        const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+        const d3 c = box_sample<COUNT>(S, P, cam, x, y, pix, s, cnt);
+        s_c[tid] = c.x;
+        s_c[kBoxAaThreads + tid] = c.y;
+        s_c[2 * kBoxAaThreads + tid] = c.z;
+    }
+    __syncthreads();
+    const uint64_t out = static_cast<uint64_t>(blockIdx.x) * ppw + tid;
+    if (tid < ppw && out < npx) {
+        d3 acc = mk(0.0, 0.0, 0.0);
+        for (int k = 0; k < aa; ++k) {
+            const int j = tid * aa + k;
+            acc = acc + mk(s_c[j], s_c[kBoxAaThreads + j], s_c[2 * kBoxAaThreads + j]);
+        }
+        store_pixel(P, static_cast<size_t>(out), sdiv(acc, static_cast<double>(aa)));
+    }
+    if constexpr (COUNT) box_count<COUNT>(cnt, P, tid);
+}
+
+// GeneratePixelAt (Scene.h:283-304) with a per-thread sample loop: single-sample frames, and
+// sample counts of 0 or above kBoxAaMax.
+template <bool COUNT, bool SINGLE>
+__global__ __launch_bounds__(kTileW * kTileH, SINGLE ? RT_BOX_WAVES : RT_BOX_MULTI_WAVES) void box_chain_kernel(TraceParams P) {
+    const uint32_t x = blockIdx.x * kTileW + threadIdx.x;
+    const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
+    Counts cnt{0u, 0u};
+    const BoxScene S = box_scene(P);
     if (x < P.width && yl < P.rows) {
         const uint32_t y = image_row(P, yl);
         const uint64_t pix = static_cast<uint64_t>(y) * P.width + x;
@@ -310,42 +395,25 @@ __global__ __launch_bounds__(kTileW * kTileH, SINGLE ? RT_BOX_WAVES : RT_BOX_MUL
         int samples = 0;
         const int nsamples = SINGLE ? 1 : P.aa;
         for (int s = 0; s < nsamples; ++s) {
-            d3 d = camera_dir(P, cam, x, y, pix, s);
-            d3 o = cam;
-            d3 c = mk(0.0, 0.0, 0.0);
-            double w = 1.0;
-            for (int depth = 0;; ++depth) {
-                if (depth >= P.max_rec) {  // TraceRay at depth maxRecursion: the sky
-                    c = c + sky(d) * w;
-                    break;
-                }
-                const Node nd = box_shade<COUNT>(S, P, o, d, cnt);
-                c = c + nd.value * w;
-                if (!nd.hit || !nd.refl) break;
-                w = w * nd.rw;
-                o = nd.ro;
-                d = nd.rd;
-            }
-            acc = acc + c;
+            acc = acc + box_sample<COUNT>(S, P, cam, x, y, pix, s, cnt);
             samples += 1;
         }
         const d3 v = samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0);
         store_pixel(P, static_cast<size_t>(yl) * P.width + x, v);
     }
-    if constexpr (COUNT) {
-        uint32_t t = cnt.trace, s = cnt.shadow;
-        for (int off = 32; off > 0; off >>= 1) {
-            t += __shfl_xor(t, off, 64);
-            s += __shfl_xor(s, off, 64);
-        }
-        if (((threadIdx.y * kTileW + threadIdx.x) & 63) == 0) {
-            atomicAdd(P.counters + 0, static_cast<unsigned long long>(t));
-            atomicAdd(P.counters + 1, static_cast<unsigned long long>(s));
-        }
-    }
+    if constexpr (COUNT) box_count<COUNT>(cnt, P, threadIdx.y * kTileW + threadIdx.x);
 }
 
-hipError_t launch_box_chain(const TraceParams& p, bool count, hipStream_t stream) {
+hipError_t launch_box_chain(const TraceParams& p, bool count, bool sample_parallel,
+                            hipStream_t stream) {
+    if (sample_parallel && p.aa >= 2 && p.aa <= kBoxAaMax) {
+        const int ppw = kBoxAaThreads / p.aa;
+        const uint64_t npx = static_cast<uint64_t>(p.width) * p.rows;
+        const dim3 grid(static_cast<unsigned>((npx + ppw - 1) / ppw));
+        if (count) hipLaunchKernelGGL((box_aa_kernel<true>), grid, dim3(kBoxAaThreads), 0, stream, p);
+        else hipLaunchKernelGGL((box_aa_kernel<false>), grid, dim3(kBoxAaThreads), 0, stream, p);
+        return hipGetLastError();
+    }
     const dim3 block(kTileW, kTileH);
     const dim3 grid((p.width + kTileW - 1) / kTileW, (p.rows + kTileH - 1) / kTileH);
     if (count) {

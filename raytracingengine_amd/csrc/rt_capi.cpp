@@ -410,7 +410,8 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
     const bool box = path == kPathChain && p.ns == 0 && p.nt == 0 && p.al_samples == 0 &&
                      p.np > 0 && !(flags & RT_FLAG_GENERIC_KERNEL);
     auto launch = [&](const TraceParams& q, bool count) {
-        if (box) return launch_box_chain(q, count, ctx->stream);
+        if (box)
+            return launch_box_chain(q, count, !(flags & RT_FLAG_NO_SAMPLE_PARALLEL), ctx->stream);
         return packet ? launch_packet_direct(q, count, sc->max_specular > 0.0, ctx->stream)
                       : (lean_generic ? lean::launch_trace(q, path, count, lds, lds_bytes, ctx->stream)
                                       : launch_trace(q, path, count, lds, lds_bytes, ctx->stream));

@@ -120,7 +120,8 @@ namespace lean {  // rt_trace_lean.hip: the same kernels for scenes without tria
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
                         hipStream_t stream);
 }
-hipError_t launch_box_chain(const TraceParams& p, bool count, hipStream_t stream);
+hipError_t launch_box_chain(const TraceParams& p, bool count, bool sample_parallel,
+                            hipStream_t stream);
 hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specular,
                                 hipStream_t stream);
 size_t packet_lds_bytes(int ns, int np, int nl);

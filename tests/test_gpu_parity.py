@@ -921,3 +921,31 @@ def test_box_chain_vs_oracle(ctx, oracle, kind):
     ref, nt, ns = oracle.render(sc)
     assert np.max(np.abs(out["hdr64"] - ref)) <= POW_TOL
     assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)
+
+
+@pytest.mark.parametrize("aa", [2, 3, 7, 32, 128, 129])
+def test_box_sample_parallel_equals_per_thread_loop(ctx, aa):
+    """Multi-sample planes-only chains run one thread per sample (rt_box.hip box_aa_kernel: 256 /
+    aa pixels per workgroup, the colours summed in sample order from LDS); the image, the ACES
+    bytes and the ray counts equal the per-thread sample loop (RT_FLAG_NO_SAMPLE_PARALLEL) and
+    the generic chain kernel bit for bit — sample counts that do not divide 256 (idle threads,
+    pixels straddling no workgroup), the largest sample-parallel count and the first above it
+    (per-thread loop either way), and a block-cyclic row set (the multi-GPU split)."""
+    from raytracingengine_amd.distributed import render_opts_for, row_ranges
+    sc = make_config("c1", 37 if aa >= 32 else 61, 23 if aa >= 32 else 45, aa=aa)
+    ds = ctx.scene(sc)
+    try:
+        out = ds.render(hdr64=True, tonemap=6, stats=True)
+        loop = ds.render(hdr64=True, tonemap=6, stats=True, flags=capi.RT_FLAG_NO_SAMPLE_PARALLEL)
+        gen = ds.render(hdr64=True, tonemap=6, stats=True, flags=capi.RT_FLAG_GENERIC_KERNEL)
+        H = sc.camera.height
+        ranges = row_ranges(1, 3, H, 4)
+        part = ds.render(hdr64=True, tonemap=6, opts=render_opts_for(ranges, 1, 3, H, 4, tonemap=6))
+    finally:
+        ds.close()
+    for ref in (loop, gen):
+        assert np.array_equal(out["hdr64"], ref["hdr64"])
+        assert np.array_equal(out["ldr"], ref["ldr"])
+        assert (out["trace_rays"], out["shadow_rays"]) == (ref["trace_rays"], ref["shadow_rays"])
+    rows = np.concatenate([out["hdr64"][a:b] for a, b in ranges])
+    assert np.array_equal(part["hdr64"], rows)

@@ -6,7 +6,7 @@ acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
         k = row["Kernel_Name"]
-        if "trace" not in k and "packet" not in k and "wf_" not in k:
+        if not any(s in k for s in ("trace", "packet", "wf_", "box_chain", "level", "fold")):
             continue
         acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
 res = {}
