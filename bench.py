@@ -447,7 +447,7 @@ def main(argv=None):
         bytes_per_launch = res["px"] * (HDR_BYTES[args.hdr] + (3 if tonemap >= 0 else 0))
         achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9
         traffic, traffic_src = load_profile(f"pmc_{config}_frames.json")
-        valu, valu_src = load_profile(f"r02_{config}_valu.json")
+        valu, valu_src = load_profile(f"r03_{config}_valu.json")
         line = {
             "metric": "Mrays/sec (primary+shadow) at 1920x1080" if config == "c2"
                       else f"Mrays/sec (primary+shadow), config {config}",
