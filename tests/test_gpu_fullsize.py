@@ -273,3 +273,23 @@ def test_moving_camera_on_two_streams(ctx):
             assert np.array_equal(bufs[k].cpu().numpy(), ref), k
     finally:
         ds.close()
+
+
+def test_full_c1_aa32_sample_parallel_equals_per_thread_loop(ctx):
+    """C1 at the reference main()'s own sampling (1000x1000, AA = 32): the sample-parallel
+    planes-only chain kernel (rt_box.hip box_aa_kernel, one thread per sample) renders the whole
+    frame, its ACES bytes and its ray counts bit-identical to the per-thread sample loop
+    (RT_FLAG_NO_SAMPLE_PARALLEL), twice (determinism)."""
+    sc = make_config("c1", aa=32)
+    ds = ctx.scene(sc)
+    try:
+        a = ds.render(hdr64=True, tonemap=ACES, stats=True)
+        b = ds.render(hdr64=True, tonemap=ACES, stats=True)
+        ref = ds.render(hdr64=True, tonemap=ACES, stats=True,
+                        flags=capi.RT_FLAG_NO_SAMPLE_PARALLEL)
+    finally:
+        ds.close()
+    for out in (a, b):
+        assert _sha(out["hdr64"]) == _sha(ref["hdr64"])
+        assert np.array_equal(out["ldr"], ref["ldr"])
+        assert (out["trace_rays"], out["shadow_rays"]) == (ref["trace_rays"], ref["shadow_rays"])
