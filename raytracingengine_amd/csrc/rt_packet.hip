@@ -70,6 +70,10 @@ constexpr int kFeatAll = 31;
 // waves/SIMD (80 VGPRs): C5 508 -> 490 us at 5 waves, -> 482 us at 6 (MI355X)
 constexpr int kFeatNoPL = 32;
 
+// Waves per SIMD of the single-sample area-only variant (C5: spheres lit by the area light)
+#ifndef RT_PACKET_AREA_WAVES
+#define RT_PACKET_AREA_WAVES 6
+#endif
 // Waves per SIMD the lean variants are compiled for (4 = at most 128 VGPRs).
 #ifndef RT_PACKET_LEAN_WAVES
 #define RT_PACKET_LEAN_WAVES 4
@@ -926,7 +930,7 @@ __device__ __forceinline__ void pk_build_image(const TraceParams& P, double* img
 }
 
 template <int MAXC, int FEAT, bool COUNT, bool MULTI, int WGY>  // MULTI = false: one sample (AA = 1)
-__global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNoPL) && !MULTI && !COUNT) ? 6 : FEAT == kFeatTris ? RT_PACKET_TRIS_WAVES : (((FEAT == 0 || (FEAT & ~kFeatNoPL) == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1)) void packet_direct_kernel(TraceParams P) {
+__global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNoPL) && !MULTI && !COUNT) ? RT_PACKET_AREA_WAVES : FEAT == kFeatTris ? RT_PACKET_TRIS_WAVES : (((FEAT == 0 || (FEAT & ~kFeatNoPL) == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1)) void packet_direct_kernel(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
     constexpr bool kNoPL = (FEAT & kFeatNoPL) != 0;  // the launcher checked P.np == P.nl == 0
