@@ -409,12 +409,13 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
     // reflection chains of scenes made of planes only take the planes-only chain kernel
     const bool box = path == kPathChain && p.ns == 0 && p.nt == 0 && p.al_samples == 0 &&
                      p.np > 0 && !(flags & RT_FLAG_GENERIC_KERNEL);
+    const bool spar = !(flags & RT_FLAG_NO_SAMPLE_PARALLEL);
     auto launch = [&](const TraceParams& q, bool count) {
         if (box)
             return launch_box_chain(q, count, !(flags & RT_FLAG_NO_SAMPLE_PARALLEL), ctx->stream);
         return packet ? launch_packet_direct(q, count, sc->max_specular > 0.0, ctx->stream)
-                      : (lean_generic ? lean::launch_trace(q, path, count, lds, lds_bytes, ctx->stream)
-                                      : launch_trace(q, path, count, lds, lds_bytes, ctx->stream));
+                      : (lean_generic ? lean::launch_trace(q, path, count, lds, lds_bytes, ctx->stream, spar)
+                                      : launch_trace(q, path, count, lds, lds_bytes, ctx->stream, spar));
     };
     // Scenes with refraction trees take the breadth-first TraceRay when the roots fit the arena
     // budget (RTAMD_WF_MB, default 4096 MiB); trees that overflow it are re-rendered per pixel.

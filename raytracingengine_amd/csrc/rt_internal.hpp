@@ -114,11 +114,14 @@ __host__ __device__ inline size_t scene_doubles(const TraceParams& p) {
            static_cast<size_t>(kLtStride) * p.nl;
 }
 
+// sample_parallel: multi-sample frames (2 ≤ aa ≤ kAaParallelMax) of the direct and chain paths
+// trace one sample per thread (rt_trace.hip), the same image as the per-thread sample loop
+constexpr int kAaParallelMax = 128;
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
-                        hipStream_t stream);
+                        hipStream_t stream, bool sample_parallel = false);
 namespace lean {  // rt_trace_lean.hip: the same kernels for scenes without triangles / area light
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
-                        hipStream_t stream);
+                        hipStream_t stream, bool sample_parallel = false);
 }
 hipError_t launch_box_chain(const TraceParams& p, bool count, bool sample_parallel,
                             hipStream_t stream);

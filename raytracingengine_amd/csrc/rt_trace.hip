@@ -32,14 +32,27 @@ namespace lean {
 // NOSPH: the scene has no spheres (C1, the reference's own box of planes): the sphere loops and
 // the sphere shading code compile away (AA = 1 chain: 80 -> 48 B/lane of spills at 3 waves/SIMD,
 // C1 489 -> 453 us on MI355X; at 4 waves it spills 224 B/lane and takes 808 us, at 5 1256 us).
-template <int PATH, bool COUNT, bool LDS, int MINW = 2, bool SINGLE = false, bool NOSPH = false>
+// SPAR: sample-parallel multi-sample frames (2 ≤ aa ≤ kAaParallelMax, direct / chain paths, never
+// the fix-up pass): thread t of the workgroup traces sample t mod aa of pixel t div aa (256 / aa
+// consecutive pixels of the row-major frame per workgroup, a 1-D grid) with the single-sample
+// code and register budget; the colours meet in LDS and one thread per pixel adds them in sample
+// order and divides by aa (GeneratePixelAt, Scene.h:292-300) — the per-thread loop's operations
+// in its order, so the same image (RT_FLAG_NO_SAMPLE_PARALLEL keeps the loop).
+template <int PATH, bool COUNT, bool LDS, int MINW = 2, bool SINGLE = false, bool NOSPH = false,
+          bool SPAR = false>
 __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParams P) {
     extern __shared__ double smem[];
+    constexpr int kThreads = kTileW * kTileH;
+    __shared__ double s_c[SPAR ? 3 * kThreads : 1];
     const int tid = threadIdx.y * kTileW + threadIdx.x;
-    const uint32_t x = blockIdx.x * kTileW + threadIdx.x;
-    const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
+    const int ppw = SPAR ? kThreads / P.aa : 1;           // pixels per workgroup (SPAR)
+    const int spl = SPAR ? tid / P.aa : 0, ss = SPAR ? tid - spl * P.aa : 0;
+    const uint64_t slin = static_cast<uint64_t>(blockIdx.x) * ppw + spl;
+    const uint32_t x = SPAR ? static_cast<uint32_t>(slin % P.width) : blockIdx.x * kTileW + threadIdx.x;
+    const uint32_t yl = SPAR ? static_cast<uint32_t>(slin / P.width) : blockIdx.y * kTileH + threadIdx.y;
     Counts cnt{0u, 0u};
-    bool run = x < P.width && yl < P.rows;
+    bool run = SPAR ? (spl < ppw && slin < static_cast<uint64_t>(P.width) * P.rows)
+                    : (x < P.width && yl < P.rows);
     if (P.redo) {  // uniform
         // fix-up pass of the wavefront renderer: only pixels with an incomplete sample tree,
         // and workgroups without one leave before staging the scene (all of them at once when
@@ -62,8 +75,9 @@ __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParam
         // GeneratePixelAt (Scene.h:283-304)
         d3 acc = mk(0.0, 0.0, 0.0);
         int samples = 0;
-        const int nsamples = SINGLE ? 1 : P.aa;
-        for (int s = 0; s < nsamples; ++s) {
+        const int nsamples = (SINGLE || SPAR) ? 1 : P.aa;
+        for (int s0 = 0; s0 < nsamples; ++s0) {
+            const int s = SPAR ? ss : s0;
             const d3 dir = camera_dir(P, cam, x, y, pix, s);
             d3 c;
             if constexpr (PATH == kPathDirect)
@@ -75,8 +89,26 @@ __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParam
             acc = acc + c;
             samples += 1;
         }
-        const d3 v = samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0);
-        store_pixel(P, static_cast<size_t>(yl) * P.width + x, v);
+        if constexpr (SPAR) {
+            s_c[tid] = acc.x;  // 0 + c: the colour as the loop's first addition makes it
+            s_c[kThreads + tid] = acc.y;
+            s_c[2 * kThreads + tid] = acc.z;
+        } else {
+            const d3 v = samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0);
+            store_pixel(P, static_cast<size_t>(yl) * P.width + x, v);
+        }
+    }
+    if constexpr (SPAR) {
+        __syncthreads();
+        const uint64_t out = static_cast<uint64_t>(blockIdx.x) * ppw + tid;
+        if (tid < ppw && out < static_cast<uint64_t>(P.width) * P.rows) {
+            d3 acc = mk(0.0, 0.0, 0.0);
+            for (int k = 0; k < P.aa; ++k) {
+                const int j = tid * P.aa + k;
+                acc = acc + mk(s_c[j], s_c[kThreads + j], s_c[2 * kThreads + j]);
+            }
+            store_pixel(P, static_cast<size_t>(out), sdiv(acc, static_cast<double>(P.aa)));
+        }
     }
     if constexpr (COUNT) {
         // wave-reduce the two counters, one 64-bit atomic per wave per counter
@@ -92,34 +124,44 @@ __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParam
     }
 }
 
-template <int PATH, bool COUNT, bool LDS, int MINW, bool SINGLE, bool NOSPH = false>
+template <int PATH, bool COUNT, bool LDS, int MINW, bool SINGLE, bool NOSPH = false,
+          bool SPAR = false>
 static hipError_t launch_one(const TraceParams& p, size_t lds_bytes, hipStream_t stream) {
     const dim3 block(kTileW, kTileH);
-    const dim3 grid((p.width + kTileW - 1) / kTileW, (p.rows + kTileH - 1) / kTileH);
-    hipLaunchKernelGGL((trace_kernel<PATH, COUNT, LDS, MINW, SINGLE, NOSPH>), grid, block,
+    dim3 grid((p.width + kTileW - 1) / kTileW, (p.rows + kTileH - 1) / kTileH);
+    if constexpr (SPAR) {  // 1-D: 256 / aa pixels per workgroup
+        const uint64_t ppw = static_cast<uint64_t>(kTileW * kTileH / p.aa);
+        grid = dim3(static_cast<unsigned>((static_cast<uint64_t>(p.width) * p.rows + ppw - 1) / ppw));
+    }
+    hipLaunchKernelGGL((trace_kernel<PATH, COUNT, LDS, MINW, SINGLE, NOSPH, SPAR>), grid, block,
                        LDS ? lds_bytes : 0, stream, p);
     return hipGetLastError();
 }
 
-template <int PATH, int MINW, bool SINGLE, bool NOSPH = false>
+template <int PATH, int MINW, bool SINGLE, bool NOSPH = false, bool SPAR = false>
 static hipError_t launch_lds(const TraceParams& p, bool count, bool lds, size_t lds_bytes,
                              hipStream_t stream) {
     if (count)
-        return lds ? launch_one<PATH, true, true, MINW, SINGLE, NOSPH>(p, lds_bytes, stream)
-                   : launch_one<PATH, true, false, MINW, SINGLE, NOSPH>(p, lds_bytes, stream);
-    return lds ? launch_one<PATH, false, true, MINW, SINGLE, NOSPH>(p, lds_bytes, stream)
-               : launch_one<PATH, false, false, MINW, SINGLE, NOSPH>(p, lds_bytes, stream);
+        return lds ? launch_one<PATH, true, true, MINW, SINGLE, NOSPH, SPAR>(p, lds_bytes, stream)
+                   : launch_one<PATH, true, false, MINW, SINGLE, NOSPH, SPAR>(p, lds_bytes, stream);
+    return lds ? launch_one<PATH, false, true, MINW, SINGLE, NOSPH, SPAR>(p, lds_bytes, stream)
+               : launch_one<PATH, false, false, MINW, SINGLE, NOSPH, SPAR>(p, lds_bytes, stream);
 }
 
 template <int PATH>
 static hipError_t launch_path(const TraceParams& p, bool count, bool lds, size_t lds_bytes,
-                              hipStream_t stream) {
+                              hipStream_t stream, bool spar) {
+    // multi-sample direct / chain frames: one thread per sample at the single-sample budget
+    const bool sp = spar && PATH != kPathTree && !p.redo && p.aa >= 2 && p.aa <= kAaParallelMax;
 #ifdef RT_LEAN_GENERIC
     // Reflection chains (C1, mirror) without triangles / area light: compiled for 3 waves/SIMD
     // (168 VGPRs; the forward-accumulated chain needs no stack) — C1 702 -> 568 us, mirror
     // 2189 -> 1684 us on MI355X; 4 waves spills 320 B/lane and loses (C1 900 us).  AA = 1 takes
     // the single-sample instantiation (80 instead of 144 B/lane of spills).
     if constexpr (PATH == kPathChain) {
+        if (sp && p.ns == 0)
+            return launch_lds<PATH, RT_CHAIN_NOSPH_WAVES, true, true, true>(p, count, lds, lds_bytes, stream);
+        if (sp) return launch_lds<PATH, 3, true, false, true>(p, count, lds, lds_bytes, stream);
         if (p.ns == 0 && p.aa == 1 && !p.redo)
             return launch_lds<PATH, RT_CHAIN_NOSPH_WAVES, true, true>(p, count, lds, lds_bytes, stream);
         if (p.aa == 1 && !p.redo) return launch_lds<PATH, 3, true>(p, count, lds, lds_bytes, stream);
@@ -128,16 +170,18 @@ static hipError_t launch_path(const TraceParams& p, bool count, bool lds, size_t
     } else
 #endif
     {
+        if constexpr (PATH != kPathTree)
+            if (sp) return launch_lds<PATH, 2, true, false, true>(p, count, lds, lds_bytes, stream);
         return launch_lds<PATH, 2, false>(p, count, lds, lds_bytes, stream);
     }
 }
 
 hipError_t launch_trace(const TraceParams& p, int path, bool count, bool lds, size_t lds_bytes,
-                        hipStream_t stream) {
+                        hipStream_t stream, bool sample_parallel) {
     switch (path) {
-    case kPathDirect: return launch_path<kPathDirect>(p, count, lds, lds_bytes, stream);
-    case kPathChain: return launch_path<kPathChain>(p, count, lds, lds_bytes, stream);
-    default: return launch_path<kPathTree>(p, count, lds, lds_bytes, stream);
+    case kPathDirect: return launch_path<kPathDirect>(p, count, lds, lds_bytes, stream, sample_parallel);
+    case kPathChain: return launch_path<kPathChain>(p, count, lds, lds_bytes, stream, sample_parallel);
+    default: return launch_path<kPathTree>(p, count, lds, lds_bytes, stream, sample_parallel);
     }
 }
 

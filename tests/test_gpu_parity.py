@@ -949,3 +949,27 @@ def test_box_sample_parallel_equals_per_thread_loop(ctx, aa):
         assert (out["trace_rays"], out["shadow_rays"]) == (ref["trace_rays"], ref["shadow_rays"])
     rows = np.concatenate([out["hdr64"][a:b] for a, b in ranges])
     assert np.array_equal(part["hdr64"], rows)
+
+
+@pytest.mark.parametrize("name,flags", [("mirror", 0), ("mesh", 0),
+                                        ("c1", capi.RT_FLAG_GENERIC_KERNEL),
+                                        ("c2", capi.RT_FLAG_GENERIC_KERNEL),
+                                        ("c5", capi.RT_FLAG_GENERIC_KERNEL)])
+@pytest.mark.parametrize("aa", [3, 32])
+def test_generic_sample_parallel_equals_per_thread_loop(ctx, name, flags, aa):
+    """Multi-sample frames of the generic direct and chain kernels (rt_trace.hip SPAR: one
+    thread per sample, the colours summed in sample order from LDS): image, ACES bytes and ray
+    counts equal the per-thread sample loop (RT_FLAG_NO_SAMPLE_PARALLEL) bit for bit — chains
+    with spheres (mirror), triangles (mesh), planes only (c1 through the generic kernel), and
+    the direct path with point lights (c2) and the area light (c5)."""
+    sc = make_config(name, 53, 29, aa=aa)
+    ds = ctx.scene(sc)
+    try:
+        out = ds.render(hdr64=True, tonemap=6, stats=True, flags=flags)
+        ref = ds.render(hdr64=True, tonemap=6, stats=True,
+                        flags=flags | capi.RT_FLAG_NO_SAMPLE_PARALLEL)
+    finally:
+        ds.close()
+    assert np.array_equal(out["hdr64"], ref["hdr64"])
+    assert np.array_equal(out["ldr"], ref["ldr"])
+    assert (out["trace_rays"], out["shadow_rays"]) == (ref["trace_rays"], ref["shadow_rays"])

@@ -66,9 +66,9 @@ def test_generic_trace_kernels_run_at_2_waves(src):
 
 
 def test_lean_chain_kernels_run_at_3_waves():
-    """trace_kernel<PATH = chain, COUNT, LDS, MINW = 3, SINGLE, NOSPH> of rt_trace_lean.hip (C1,
-    mirror; NOSPH: the sphere-free instantiations C1 takes)."""
+    """trace_kernel<PATH = chain, COUNT, LDS, MINW = 3, SINGLE, NOSPH, SPAR> of rt_trace_lean.hip
+    (C1, mirror; NOSPH: the sphere-free instantiations C1 takes; SPAR: one thread per sample)."""
     ks = _kernels("rt_trace_lean.hip")
     chain = {n: r for n, r in ks.items() if re.search(r"trace_kernelILi1ELb[01]ELb[01]ELi3E", n)}
-    assert len(chain) == 16, sorted(ks)
+    assert len(chain) == 24, sorted(ks)
     assert all(_waves(r) >= 3 for r in chain.values()), chain
