@@ -506,6 +506,16 @@ def main(argv=None):
                     "note": "the same frames through the C-ABI serving queue (rt_queue), "
                             "several in flight on separate HIP streams; serving throughput, "
                             "not the headline value"}
+            # BASELINE config 1: the reference main()'s own scene and sampling
+            sc1 = make_config("c1", aa=32)
+            c1 = frames_mode(R, sc1, 10, 2, "f64", R.capi.TONEMAPS.index("aces"), 0)
+            line["reference_main_c1"] = {
+                "workload": "c1: the reference main() box (5 mirrored axis planes, 2 point "
+                            "lights), 1000x1000, AA=32, f64 Vec3 HDR + fused ACES u8",
+                "ms_per_frame": round(c1["elapsed"] / 10 * 1e3, 4),
+                "kernel_ms_per_launch": round(c1["region_ms"], 4),
+                "rays_per_frame": c1["rays"],
+                "value": round(c1["rays"] * 10 / c1["elapsed"] / 1e6, 3), "unit": "Mrays/s"}
             line["d2h"] = d2h_frames(R, sc, min(args.steps, 20), tonemap)
             # the N>1 default workload (C4 tiled + RCCL gather) on this one GPU
             sc4 = make_config("c4", aa=1)
