@@ -70,6 +70,12 @@ constexpr int kFeatAll = 31;
 // waves/SIMD (80 VGPRs): C5 508 -> 490 us at 5 waves, -> 482 us at 6 (MI355X)
 constexpr int kFeatNoPL = 32;
 
+// Waves per SIMD of the single-sample variant for <= 64 spheres, point lights and no other
+// feature (C2): 6 with its light records read through the scalar cache (80 VGPRs, 48 B/lane of
+// scratch): C2 48.1 -> 46.7 us against 5 waves (95 VGPRs + 20 B, lights from LDS), MI355X
+#ifndef RT_PACKET_SMALL_WAVES
+#define RT_PACKET_SMALL_WAVES 6
+#endif
 // Waves per SIMD of the single-sample area-only variant (C5: spheres lit by the area light)
 #ifndef RT_PACKET_AREA_WAVES
 #define RT_PACKET_AREA_WAVES 6
@@ -848,6 +854,25 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     }
 }
 
+// Point light l's position and E = colour·intensity.  With <= 64 spheres (MAXC == 1) the record
+// is read through the scalar cache: wave-uniform, so SGPRs instead of VGPRs, which is what lets
+// C2's variant run at 6 waves/SIMD (RT_PACKET_SMALL_WAVES).  More spheres keep the LDS copy
+// (C3 +1.2 % through the scalar cache: the chunk masks need those SGPRs).
+typedef const __attribute__((address_space(4))) double* pk_cdp;
+template <int MAXC>
+__device__ __forceinline__ void pk_light_record(const PacketScene& S, const TraceParams& P, int l,
+                                                d3& L, d3& E) {
+    if constexpr (MAXC == 1) {
+        const pk_cdp q = (pk_cdp)P.lt + kLtStride * l;
+        L = mk(q[0], q[1], q[2]);
+        E = mk(q[3], q[4], q[5]);
+    } else {
+        const double* q = S.lt + kLtStride * l;
+        L = mk(q[0], q[1], q[2]);
+        E = mk(q[3], q[4], q[5]);
+    }
+}
+
 // The packet kernel's LDS image of a scene seen from one camera (layout below, 16-byte
 // aligned arrays): spheres, camera-cone terms, culling radii, camera-ray sphere constants,
 // planes with their camera numerators, point lights, camera-ray plane normals.  Formed by each
@@ -930,7 +955,7 @@ __device__ __forceinline__ void pk_build_image(const TraceParams& P, double* img
 }
 
 template <int MAXC, int FEAT, bool COUNT, bool MULTI, int WGY>  // MULTI = false: one sample (AA = 1)
-__global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNoPL) && !MULTI && !COUNT) ? RT_PACKET_AREA_WAVES : FEAT == kFeatTris ? RT_PACKET_TRIS_WAVES : (((FEAT == 0 || (FEAT & ~kFeatNoPL) == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1)) void packet_direct_kernel(TraceParams P) {
+__global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !MULTI && !COUNT) ? RT_PACKET_SMALL_WAVES : (FEAT == (kFeatArea | kFeatNoPL) && !MULTI && !COUNT) ? RT_PACKET_AREA_WAVES : FEAT == kFeatTris ? RT_PACKET_TRIS_WAVES : (((FEAT == 0 || (FEAT & ~kFeatNoPL) == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1)) void packet_direct_kernel(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
     constexpr bool kNoPL = (FEAT & kFeatNoPL) != 0;  // the launcher checked P.np == P.nl == 0
@@ -1119,10 +1144,10 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == (kFeatArea | kFeatNo
             }
             d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
             for (int l = 0; l < nl; ++l) {
-                const double* lp = S.lt + kLtStride * l;
-                const d3 L = mk(lp[0], lp[1], lp[2]);
-                pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, L, mk(lp[3], lp[4], lp[5]),
-                                            L, 0.0, bias, nchunks, diff, spec, cnt);
+                d3 L, E;
+                pk_light_record<MAXC>(S, P, l, L, E);
+                pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, L, E, L, 0.0, bias, nchunks,
+                                            diff, spec, cnt);
             }
             if constexpr ((FEAT & kFeatArea) != 0) {
                 if (P.al_samples > 0) {

@@ -1,7 +1,7 @@
 """Register budgets of the built gfx950 kernels (CPU: reads the code objects' metadata).
 
 Occupancy is the lever measured most in DESIGN.md §4: the single-sample packet kernels run at
-5 waves/SIMD (≤ 96 VGPRs + AGPRs; the area-only one at 6, ≤ 80), the lean reflection-chain kernels at 3 (≤ 168: C1 -19 %,
+5 waves/SIMD (≤ 96 VGPRs + AGPRs; C2's and the area-only one at 6, ≤ 80), the lean reflection-chain kernels at 3 (≤ 168: C1 -19 %,
 mirror -23 % against 2) and the other generic / breadth-first trace kernels at 2 (≤ 256).
 An unrelated change once pushed the breadth-first level kernel into AGPRs and 1 wave/SIMD
 (glass +35 %); this pins the budgets on the objects `build()` produced."""
@@ -52,6 +52,9 @@ def test_packet_single_sample_kernels_run_at_5_waves():
             if re.search(r"packet_direct_kernelILi[14]ELi(0|2|16|34)ELb0ELb0E", n)}
     assert len(lean) == 14, sorted(lean)
     assert all(_waves(r) >= 5 for r in lean.values()), lean
+    # <= 64 spheres and point lights only (C2): 6, its light records read through the scalar cache
+    small = {n: r for n, r in lean.items() if re.search(r"packet_direct_kernelILi1ELi0ELb0ELb0E", n)}
+    assert small and all(_waves(r) >= 6 for r in small.values()), small
     # the area-only variant (FEAT 34 = area light, no planes / point lights: C5) runs at 6
     area_only = {n: r for n, r in lean.items() if "ELi34E" in n}
     assert len(area_only) == 2 and all(_waves(r) >= 6 for r in area_only.values()), area_only
