@@ -1,33 +1,35 @@
 #!/usr/bin/env python3
 """Headline benchmark: Mrays/s (primary+shadow) of the per-pixel trace at 1920×1080 (BASELINE
-config 2: 16 spheres + 2 planes + 1 point light, Reinhard tonemap) on 1..N MI355X.
+config 2: 16 spheres + 2 planes + 1 point light, Reinhard tonemap) on 1, 2, 4 or 8 MI355X.
 
 Contract (driver):  python bench.py --gpus N --steps K --warmup W
   * N=1 runs in-process; N>1 is launched by torch.distributed.run, one rank per GPU.
-  * N=1 (mode "frames"): a step = one pass of the hot path over one frame — Scene::RenderImage()
-    of the C2 frame into the float64 Vec3 framebuffer + the fused Reinhard tonemap to uint8
-    (RaytracingEngine.cpp:133), everything resident in HBM (scene uploaded once, outputs stay
-    on the device).
-  * N>1 (mode "tiled", BASELINE config 4 / SURVEY §8e): a step = ONE 7680×4320 C4 frame split
-    into block-cyclic row sets over the ranks, each rank renders its rows (fused Reinhard
-    uint8), ONE RCCL gather (ncclGather over xGMI, behind the C-ABI: rt_render_gather) moves
-    them to rank 0, and rank 0 assembles the frame in image order in its device framebuffer.
-    Strong scaling; the per-rank render / gather / assembly times are in the line, and the
-    weak-scaling C2 frames throughput is an extra field (`weak_frames`).
-  * Untimed steps for --clock-warmup-ms (default 50 ms) of wall time so the GPU is at its
+  * The SAME workload and code path at every N (RE/Scene.h:318-325): a step = one
+    C2 frame — Scene::RenderImage() into the float64 Vec3 framebuffer + the fused Reinhard bytes
+    (RaytracingEngine.cpp:133), everything resident in HBM — split into block-cyclic 16-row
+    blocks over the N ranks.  Every rank renders its rows (f64 HDR rows kept on the rank, the
+    bytes into its send buffer), ONE ncclGather per frame moves the bytes to rank 0 over xGMI,
+    and rank 0 writes them into image order (rt_render_gather_batch).  At N=1 the one rank's
+    rows are the frame: it renders straight into the frame buffers, nothing to gather.
+  * Frames go in batches of --batch (default 8) per call: one render launch per batch (one
+    grid plane per frame, so a small per-rank share of a frame does not pay a whole launch's
+    ramp and drain), the batch's ncclGathers in one ncclGroup, one assembly launch; two
+    batches in flight (RT_FLAG_PIPELINE: batch b's gather overlaps batch b+1's render).
+  * Untimed frames for --clock-warmup-ms (default 50 ms) of wall time so the GPU is at its
     sustained clock (it needs ~30 ms of load to leave idle: 143 → 45 µs per C2 frame,
-    tools/clock_ramp.py), then W untimed steps, then exactly K timed steps bracketed by
+    tools/clock_ramp.py), then W untimed frames, then exactly K timed frames bracketed by
     barrier + synchronize on both sides; the max over ranks is the time; rank 0 prints ONE
     JSON line.
 
-Extra fields (N=1): `roofline` (HBM-write bound of the trace kernel from live per-launch HIP
-events; traffic and VALU counters from the committed PMC summaries), `roofline_f32` (the same
-launch with the north star's float3 framebuffer), `moving_camera` (a new camera position every
-frame: no cached per-camera packet image), `d2h` (frames/s of the synchronous host-buffer
-render, the drop-in RenderImage()'s path, pageable and pinned), `tiled_1gpu` (the N>1 default
-workload on one GPU through the same gather path: the strong-scaling anchor), `pipelined` (the
-same frames through the C-ABI serving queue rt_queue, 2 in flight), `cpu_baseline`
-(the unmodified reference renderer, oracle/_ref, timed on this host's cores).
+Extra fields (each outside the headline's timed region, with its own timing): `per_rank`
+(render / gather / assembly per frame on every rank), `roofline` (HBM-write bound of the trace
+kernel from live per-launch HIP events; traffic and VALU counters from the committed PMC
+summaries), `single_launch` (one launch per frame, the round-3 headline path), `weak_frames`
+(every rank its own whole frames), `c4_tiled` (BASELINE config 4: the 7680×4320 frame through
+the same path), and at N=1 `roofline_f32` (the north star's float3 framebuffer),
+`moving_camera` (a new camera position every frame), `d2h` (the drop-in RenderImage() with
+its device-to-host copy), `reference_main_c1` (BASELINE config 1 as the reference main()
+renders it) and `cpu_baseline` (the unmodified reference renderer, oracle/_ref, on this host).
 """
 from __future__ import annotations
 
@@ -42,40 +44,33 @@ sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
 HDR_BYTES = {"f64": 24, "f32": 12}
-GATHER_OUT = {"u8": ("RT_OUT_LDR", 3), "f32": ("RT_OUT_HDR32", 12), "f64": ("RT_OUT_HDR64", 24)}
 
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default=None,
-                    help="c1..c5 (BASELINE configs), mirror, glass, mesh; default c2 (frames), "
-                         "c4 (tiled)")
-    ap.add_argument("--mode", choices=["frames", "tiled"], default=None,
-                    help="default: frames at N=1, tiled at N>1")
+    ap.add_argument("--steps", type=int, default=200, help="timed frames")
+    ap.add_argument("--warmup", type=int, default=20, help="untimed frames after the clock warm-up")
+    ap.add_argument("--config", default="c2",
+                    help="c1..c5 (BASELINE configs), mirror, glass, mesh, bigmesh; default c2")
+    ap.add_argument("--batch", type=int, default=8,
+                    help="frames per rt_render_gather_batch call (1..16 per launch)")
     ap.add_argument("--tonemap", default="reinhard_simple",
-                    help="fused LDR operator, or 'none' (HDR only)")
+                    help="fused LDR operator (the gathered bytes)")
     ap.add_argument("--row-block", type=int, default=16,
-                    help="tiled mode: rows per block of the block-cyclic split")
-    ap.add_argument("--gather", choices=sorted(GATHER_OUT), default="u8",
-                    help="tiled mode: the framebuffer each rank renders and rank 0 gathers")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="tiled mode: gather on the render stream (no overlap of frame k's "
-                         "gather with frame k+1's render)")
+                    help="rows per block of the block-cyclic split (N>1)")
     ap.add_argument("--hdr", choices=["f64", "f32"], default="f64",
-                    help="frames mode HDR framebuffer: f64 = the reference's std::vector<Vec3>")
+                    help="the rank-local HDR framebuffer: f64 = the reference's std::vector<Vec3>")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="gather on the render stream (no overlap of batch b's gather with "
+                         "batch b+1's render)")
     ap.add_argument("--clock-warmup-ms", type=float, default=50.0,
-                    help="untimed steps for this much wall time before the W warmup steps, so "
-                         "that the K timed steps run at the GPU's sustained clock")
-    ap.add_argument("--event-every", type=int, default=10,
-                    help="bracket every n-th timed step with HIP events (0: none)")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="> 1: also measure the frames with this many in flight through the "
-                         "C-ABI serving queue, rt_queue ('pipelined' field; N=1 extras)")
+                    help="untimed frames for this much wall time before the W warmup frames, so "
+                         "that the K timed frames run at the GPU's sustained clock")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="bracket every n-th timed batch with HIP events (0: none)")
     ap.add_argument("--no-extras", action="store_true",
-                    help="headline only (no f32 / moving-camera / D2H / tiled / weak fields)")
+                    help="headline only (no extra fields)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=6,
                     help="reference frames timed for cpu_baseline (first one is warm-up)")
@@ -144,7 +139,8 @@ def cpu_baseline(sc, rays_per_frame: int, frames: int):
 
 
 class Runner:
-    """Per-process state: the rank, a torch stream the library launches on, timing helpers."""
+    """Per-process state: the rank, a torch stream the library launches on, the rank's
+    communicator (a one-rank RCCL communicator at N=1), timing helpers."""
 
     def __init__(self, args):
         import torch
@@ -164,6 +160,29 @@ class Runner:
         self.ctx = capi.Context(self.local_rank)
         self.stream = torch.cuda.Stream()
         self.ctx.set_stream(self.stream.cuda_stream)
+        if self.world > 1:
+            uid = [capi.comm_unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            uid = uid[0]
+        else:
+            uid = capi.comm_unique_id()
+        self.comm = capi.Comm(self.ctx, self.world, self.rank, uid)
+
+    def solo_comm(self):
+        """A one-rank communicator on this GPU (every rank its own whole frames)."""
+        if self.world == 1:
+            return self.comm
+        if not hasattr(self, "_solo"):
+            self._solo = self.capi.Comm(self.ctx, 1, 0, self.capi.comm_unique_id())
+        return self._solo
+
+    def close(self):
+        if hasattr(self, "_solo"):
+            self._solo.close()
+        self.comm.close()
+        self.ctx.close()
+        if self.world > 1:
+            self.dist.destroy_process_group()
 
     def barrier(self):
         if self.world > 1:
@@ -192,24 +211,29 @@ class Runner:
         self.dist.all_gather(out, t)
         return [[float(x) for x in o] for o in out]
 
-    def timed(self, step, steps, warmup, region_events=True, warm_step=None):
-        """Untimed steps for `--clock-warmup-ms` of wall time (the GPU leaves its idle clock
-        only after ~30 ms of sustained load: tools/clock_ramp.py, C2 143 → 54 → 45 µs/frame
-        over the first 30 ms), then W untimed steps, then K timed steps between barrier +
-        synchronize; returns (elapsed seconds max over ranks, HIP-event region ms per step on
-        the launch stream).  `warm_step` (default `step`) is what the clock warm-up runs: it
-        must not be a collective, since each rank warms up for its own wall time."""
+    def timed(self, step, frames, warmup, batch, warm_step=None, region_events=False):
+        """Untimed work for `--clock-warmup-ms` of wall time (the GPU leaves its idle clock only
+        after ~30 ms of sustained load: tools/clock_ramp.py, C2 143 → 54 → 45 µs/frame over the
+        first 30 ms), then `warmup` untimed frames, then `frames` timed frames between barrier +
+        synchronize.  step(first_frame, nframes, timed) enqueues nframes frames (≤ batch).
+        Returns (elapsed seconds max over ranks, HIP-event region ms on the launch stream).
+        `warm_step` (default `step`) is what the clock warm-up runs: it must not be a
+        collective, since each rank warms up for its own wall time."""
         torch = self.torch
         warm = warm_step or step
         t_end = time.perf_counter() + self.args.clock_warmup_ms / 1e3
         k = 0
         while time.perf_counter() < t_end:
-            for _ in range(16):
-                warm(-1000000 - k, False)
-                k += 1
+            for _ in range(4):
+                warm(-1000000 - k, batch, False)
+                k += batch
             torch.cuda.synchronize()
-        for i in range(warmup):
-            step(i, False)
+
+        def run(n, timed):
+            for f0 in range(0, n, batch):
+                step(f0, min(batch, n - f0), timed)
+
+        run(warmup, False)
         # drain this rank's work (its RCCL gathers included) before the process group's own
         # collective: two communicators' kernels are never in flight together
         torch.cuda.synchronize()
@@ -218,13 +242,12 @@ class Runner:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(self.stream)   # on the stream the trace kernel is launched on
-        for i in range(steps):
-            step(i, True)
+        run(frames, True)
         ev1.record(self.stream)
         torch.cuda.synchronize()
         self.barrier()
         elapsed = time.perf_counter() - t0
-        region_ms = ev0.elapsed_time(ev1) / steps if region_events else None
+        region_ms = ev0.elapsed_time(ev1) if region_events else None
         (elapsed,) = self.max_over_ranks(elapsed)
         return elapsed, region_ms
 
@@ -247,65 +270,116 @@ class Runner:
             self.ctx.reset_stats()
         return st.trace_rays + st.shadow_rays
 
+    def rank_plan(self, H, block):
+        """rt_render_opts of this rank's block-cyclic rows (its share of every frame)."""
+        o = self.capi.default_opts(tonemap=-1)
+        if self.world > 1:
+            o.row_begin, o.row_end = self.rank * block, H
+            o.row_block, o.row_cycle = block, self.world
+        return o
 
-# ------------------------------------------------------------------------------ frames mode
-def frames_mode(R: Runner, sc, steps, warmup, hdr="f64", tonemap=1, event_every=10,
-                camera_step=None):
-    """Every rank renders whole frames (weak scaling).  camera_step(i) -> new camera position
-    per frame (moving camera), else a static camera."""
+
+# ------------------------------------------------------------------------------ the headline
+def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, block=16,
+                 pipeline=True, event_every=4, camera_step=None, gather=True):
+    """Frames of `sc` split over the ranks (block-cyclic rows), `batch` frames per
+    rt_render_gather_batch call: this rank's rows of the HDR framebuffer stay on the rank, the
+    fused bytes are gathered to rank 0 (one ncclGather per frame; none at N=1) and assembled.
+    gather=False: every rank renders whole frames of its own (weak scaling; same call on a
+    one-rank view).  camera_step(base, frame) -> a new camera position per frame."""
     torch, capi = R.torch, R.capi
     W, H = sc.camera.width, sc.camera.height
     dscene = R.ctx.scene(sc)
-    hdr_t = torch.empty(H * W * 3, dtype=torch.float64 if hdr == "f64" else torch.float32,
-                        device="cuda")
-    ldr = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda") if tonemap >= 0 else None
-    hargs = (hdr_t.data_ptr(), None) if hdr == "f64" else (None, hdr_t.data_ptr())
-    opts = capi.default_opts(tonemap=tonemap)
-    timed_opts = capi.default_opts(tonemap=tonemap, flags=capi.RT_FLAG_TIME_KERNEL)
-    rays = R.count_rays(dscene, opts)
+    split = gather and R.world > 1
+    plan = R.rank_plan(H, block) if split else capi.default_opts(tonemap=-1)
+    rows = capi.rendered_rows(plan, H) if plan.row_begin < H else 0
+    rays_rank = R.count_rays(dscene, plan) if rows else 0
+    comm = R.comm if split else R.solo_comm()
+    # two sets of buffers (the pipelined slots): batch b writes set b mod 2
+    hdr_dtype = torch.float64 if hdr == "f64" else torch.float32
+    local = [torch.empty(max(rows, 1) * W * 3 * batch, dtype=hdr_dtype, device="cuda")
+             for _ in range(2)]
+    root = R.rank == 0 or not split
+    ldr = [torch.empty(H * W * 3 * batch if root else 1, dtype=torch.uint8, device="cuda")
+           for _ in range(2)]
+    pf = capi.RT_FLAG_PIPELINE if pipeline else 0
+    opts = capi.default_opts(tonemap=tonemap, row_block=block if split else 0, flags=pf)
+    topts = capi.default_opts(tonemap=tonemap, row_block=block if split else 0,
+                              flags=pf | capi.RT_FLAG_TIME_KERNEL)
     base = dscene.camera["position"][0].copy()
+    static_cams = dscene.cameras([base] * batch)
+    nb = [0]
 
-    def step(i, timed):
-        if camera_step is not None:
-            dscene.camera["position"][0] = camera_step(base, i if timed else -1 - i)
-        ev = timed and event_every > 0 and i % event_every == 0
-        dscene.render_device(*hargs, ldr.data_ptr() if ldr is not None else None,
-                             timed_opts if ev else opts)
+    def cams_for(f0, n):
+        if camera_step is None:
+            return static_cams[:n]
+        return dscene.cameras([camera_step(base, f0 + j) for j in range(n)])
 
-    R.ctx.reset_stats()
-    elapsed, region_ms = R.timed(step, steps, warmup)
-    kst = R.ctx.stats()
-    dscene.camera["position"][0] = base
+    def step(f0, n, timed):
+        b = nb[0]
+        nb[0] += 1
+        ev = timed and event_every > 0 and b % event_every == 0
+        kw = {"rank_hdr64": local[b & 1].data_ptr()} if hdr == "f64" else \
+             {"rank_hdr32": local[b & 1].data_ptr()}
+        comm.render_gather_batch(dscene, cams_for(f0, n), topts if ev else opts, capi.RT_OUT_LDR,
+                                 d_ldr=ldr[b & 1].data_ptr(), **kw)
+
+    # the clock warm-up renders this rank's rows without the gather (no collective)
+    wopts = capi.default_opts(tonemap=tonemap)
+    for f, _ in capi.RenderOpts._fields_:
+        if f.startswith("row_"):
+            setattr(wopts, f, getattr(plan, f))
+
+    def warm_step(f0, n, timed):
+        if rows:
+            dscene.render_batch(static_cams[:n], local[0].data_ptr() if hdr == "f64" else None,
+                                local[0].data_ptr() if hdr == "f32" else None,
+                                ldr[0].data_ptr() if root else local[1].data_ptr(), wopts)
+
+    comm.timing(reset=True)
+    elapsed, _ = R.timed(step, frames, warmup, batch, warm_step=warm_step if split else None)
+    t = comm.timing(reset=True)
+    per_frame = [t.render_ms / max(t.frames, 1), t.gather_ms / max(t.frames, 1),
+                 t.assemble_ms / max(t.frames, 1), float(rows), float(rays_rank), float(t.frames)]
+    ranks = R.gather_rows(per_frame)
+    (rays_all,) = R.sum_over_ranks(float(rays_rank))
     dscene.close()
-    sampled_ms = kst.kernel_ms / kst.launches if kst.launches else None
-    return {"rays": rays, "elapsed": elapsed, "region_ms": region_ms, "sampled_ms": sampled_ms,
-            "px": W * H, "bufs": (hdr_t, ldr)}
+    return {"elapsed": elapsed, "rays": rays_all, "rays_rank": rays_rank, "ranks": ranks,
+            "px": W * H, "rows": rows, "frames": frames, "batch": batch,
+            "bufs": (local, ldr)}
 
 
-def pipelined_frames(R: Runner, sc, steps, warmup, inflight, tonemap=1):
-    """The same K frames through the C-ABI serving queue (rt_queue): `inflight` frames in flight
-    on as many HIP streams, each with its own framebuffers — one frame's launch tail overlaps the
-    next frame's start."""
+def per_rank_summary(res):
+    ranks = res["ranks"]
+    render = [r[0] for r in ranks]
+    mean = sum(render) / len(render)
+    return {
+        "per_rank": [{"rank": i, "rows": int(r[3]), "rays_per_frame": int(r[4]),
+                      "render_ms_per_frame": round(r[0], 6), "gather_ms_per_frame": round(r[1], 6),
+                      "assemble_ms_per_frame": round(r[2], 6), "timed_frames": int(r[5])}
+                     for i, r in enumerate(ranks)],
+        "render_imbalance": round(max(render) / mean, 4) if mean > 0 else None,
+    }
+
+
+def single_launch_frames(R: Runner, sc, frames, warmup, tonemap=1):
+    """One launch per frame (rt_render_device of the whole frame, f64 + bytes), the round-3
+    headline path: returns (Mrays/s, ms per frame, HIP-event ms per launch)."""
     torch, capi = R.torch, R.capi
     W, H = sc.camera.width, sc.camera.height
     dscene = R.ctx.scene(sc)
-    q = capi.Queue(R.ctx, inflight)
-    bufs = [(torch.empty(H * W * 3, dtype=torch.float64, device="cuda"),
-             torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")) for _ in range(inflight)]
+    h = torch.empty(H * W * 3, dtype=torch.float64, device="cuda")
+    l = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")
     opts = capi.default_opts(tonemap=tonemap)
+    rays = R.count_rays(dscene, opts)
 
-    def step(i, timed):
-        # frame i goes to slot i mod depth: the queue's stream order keeps a slot's frames in
-        # order, so its framebuffers are rewritten only after the previous frame wrote them (a
-        # consumer would rt_queue_wait(ticket) before reading; nothing here reads them)
-        h, l = bufs[i % inflight]
-        q.submit(dscene, opts, h.data_ptr(), None, l.data_ptr())
+    def step(f0, n, timed):
+        for _ in range(n):
+            dscene.render_device(h.data_ptr(), None, l.data_ptr(), opts)
 
-    elapsed, _ = R.timed(step, steps, warmup, region_events=False)
-    q.synchronize()
-    q.close()
+    elapsed, region = R.timed(step, frames, warmup, 1, region_events=True)
     dscene.close()
-    return elapsed
+    return rays * frames / elapsed / 1e6, elapsed / frames * 1e3, region / frames
 
 
 def d2h_frames(R: Runner, sc, frames=20, tonemap=1):
@@ -338,88 +412,14 @@ def d2h_frames(R: Runner, sc, frames=20, tonemap=1):
     return out
 
 
-# ------------------------------------------------------------------------------ tiled mode
-def tiled_mode(R: Runner, sc, steps, warmup, gather="u8", tonemap=1, block=16,
-               event_every=10, pipeline=True):
-    """One frame split over the ranks: block-cyclic rows, one RCCL gather to rank 0, rank 0
-    assembles the frame in image order (rt_render_gather).  Returns per-rank timings."""
-    torch, capi = R.torch, R.capi
+def workload_text(sc, world, block, batch, hdr, tonemap_name):
     W, H = sc.camera.width, sc.camera.height
-    if R.world > 1:
-        uid = [capi.comm_unique_id() if R.rank == 0 else None]
-        R.dist.broadcast_object_list(uid, src=0)
-        uid = uid[0]
-    else:
-        uid = capi.comm_unique_id()
-    comm = capi.Comm(R.ctx, R.world, R.rank, uid)
-    dscene = R.ctx.scene(sc)
-    out_name, bpp = GATHER_OUT[gather]
-    outputs = getattr(capi, out_name)
-    dtype = {"u8": torch.uint8, "f32": torch.float32, "f64": torch.float64}[gather]
-    frame = torch.empty(H * W * 3 if R.rank == 0 else 1, dtype=dtype, device="cuda")
-    ptrs = [None, None, None]
-    if R.rank == 0:
-        ptrs[{"f64": 0, "f32": 1, "u8": 2}[gather]] = frame.data_ptr()
-    tm = tonemap if gather == "u8" else -1
-    pf = capi.RT_FLAG_PIPELINE if pipeline else 0
-    opts = capi.default_opts(tonemap=tm, row_block=block, flags=pf)
-    timed_opts = capi.default_opts(tonemap=tm, row_block=block,
-                                   flags=pf | capi.RT_FLAG_TIME_KERNEL)
-    # this rank's rays: its rows of the frame (the gather's plan)
-    plan = capi.default_opts(tonemap=-1)
-    if R.world > 1:
-        plan.row_begin, plan.row_end = R.rank * block, H
-        plan.row_block, plan.row_cycle = block, R.world
-    rays_rank = R.count_rays(dscene, plan) if plan.row_begin < H else 0
-
-    def step(i, timed):
-        ev = timed and event_every > 0 and i % event_every == 0
-        comm.render_gather(dscene, timed_opts if ev else opts, outputs, *ptrs)
-
-    # the clock warm-up renders this rank's rows without the gather (no collective)
-    wopts = capi.default_opts(tonemap=tm)
-    for f, _ in capi.RenderOpts._fields_:
-        if f.startswith("row_"):
-            setattr(wopts, f, getattr(plan, f))
-    wrows = capi.rendered_rows(wopts, H) if wopts.row_begin < H else 0
-    wbuf = torch.empty(max(wrows, 1) * W * bpp, dtype=torch.uint8, device="cuda")
-    wptrs = [None, None, None]
-    wptrs[{"f64": 0, "f32": 1, "u8": 2}[gather]] = wbuf.data_ptr()
-
-    def warm_step(i, timed):
-        if wrows:
-            dscene.render_device(*wptrs, wopts)
-
-    comm.timing(reset=True)
-    elapsed, _ = R.timed(step, steps, warmup, region_events=False, warm_step=warm_step)
-    t = comm.timing(reset=True)
-    per = [t.render_ms / max(t.frames, 1), t.gather_ms / max(t.frames, 1),
-           t.assemble_ms / max(t.frames, 1), float(t.rows), float(rays_rank)]
-    ranks = R.gather_rows(per)
-    (rays_all,) = R.sum_over_ranks(float(rays_rank))
-    dscene.close()
-    comm.close()
-    return {"elapsed": elapsed, "rays": rays_all, "ranks": ranks, "px": W * H, "bpp": bpp,
-            "max_rows": t.max_rows, "pipeline": pipeline}
-
-
-def tiled_summary(res, steps, W, gather, block):
-    ranks = res["ranks"]
-    render = [r[0] for r in ranks]
-    mean_render = sum(render) / len(render)
-    return {
-        "per_rank": [{"rank": i, "rows": int(r[3]), "rays": int(r[4]), "render_ms": round(r[0], 5),
-                      "gather_ms": round(r[1], 5), "assemble_ms": round(r[2], 5)}
-                     for i, r in enumerate(ranks)],
-        "render_ms_max": round(max(render), 5),
-        "render_imbalance": round(max(render) / mean_render, 4) if mean_render > 0 else None,
-        "gather_bytes_per_rank": res["max_rows"] * W * res["bpp"],
-        "gathered": gather,
-        "row_block": block,
-        "pipelined": res["pipeline"],
-        "ms_per_frame": round(res["elapsed"] / steps * 1e3, 5),
-        "value": round(res["rays"] * steps / res["elapsed"] / 1e6, 3),
-    }
+    return (f"{sc.name}: {W}x{H}, {len(sc.spheres)} spheres, {len(sc.planes)} planes, "
+            f"{len(sc.lights)} point lights, AA=1, static camera; a step = one frame: every "
+            f"rank renders its block-cyclic {block}-row blocks ({hdr} Vec3 HDR rows kept on the "
+            f"rank + fused {tonemap_name} u8), one ncclGather per frame moves the u8 rows to "
+            f"rank 0, which assembles the frame (N=1: the one rank renders the whole frame "
+            f"straight into it); {batch} frames per call")
 
 
 # ------------------------------------------------------------------------------ main
@@ -429,158 +429,125 @@ def main(argv=None):
     capi = R.capi
     from raytracingengine_amd.configs import make_config
 
-    mode = args.mode or ("frames" if R.world == 1 else "tiled")
-    config = args.config or ("c2" if mode == "frames" else "c4")
-    tonemap = -1 if args.tonemap == "none" else capi.TONEMAPS.index(args.tonemap)
-    sc = make_config(config, aa=1)
+    tonemap = capi.TONEMAPS.index(args.tonemap)
+    sc = make_config(args.config, aa=1)
     W, H = sc.camera.width, sc.camera.height
-    line = None
     extras = not args.no_extras
+    batch = max(1, args.batch)
 
-    if mode == "frames":
-        res = frames_mode(R, sc, args.steps, args.warmup, args.hdr, tonemap, args.event_every)
-        elapsed, rays_rank = res["elapsed"], res["rays"]
-        (kernel_ms,) = R.max_over_ranks(res["region_ms"])
-        (rays_all,) = R.sum_over_ranks(float(rays_rank))
-        value = rays_all * args.steps / elapsed / 1e6
-        frames = R.world * args.steps
-        bytes_per_launch = res["px"] * (HDR_BYTES[args.hdr] + (3 if tonemap >= 0 else 0))
-        achieved = bytes_per_launch / (kernel_ms / 1e3) / 1e9
-        traffic, traffic_src = load_profile(f"pmc_{config}_frames.json")
-        valu, valu_src = load_profile(f"r03_{config}_valu.json")
-        line = {
-            "metric": "Mrays/sec (primary+shadow) at 1920x1080" if config == "c2"
-                      else f"Mrays/sec (primary+shadow), config {config}",
-            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": R.world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic",
-            "config": {
-                "workload": f"{config}: {W}x{H}, {len(sc.spheres)} spheres, {len(sc.planes)} "
-                            f"planes, {len(sc.lights)} point lights, AA=1, {args.hdr} Vec3 HDR "
-                            f"framebuffer + fused {args.tonemap} u8, static camera",
-                "global_batch": frames, "resolution": [W, H],
-                "parallelism": f"frames x{R.world}", "rays_per_frame": rays_rank,
-            },
-            "frames_per_sec": round(frames / elapsed, 3),
-            "clock_warmup_ms": args.clock_warmup_ms,
-            "kernel_ms_per_launch": round(kernel_ms, 6),
-            "kernel_ms_sampled_events": round(res["sampled_ms"], 6) if res["sampled_ms"] else None,
-            "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
-                "alg_bytes_per_launch": bytes_per_launch, "traffic_source": traffic_src,
-            },
-            "valu": valu, "valu_source": valu_src,
-            "cpu_baseline": None,
-        }
-        if extras and R.world == 1:
-            steps_x = min(args.steps, 100)
-            # the north star's float3 framebuffer (+ u8): 15 B/px instead of 27
-            f32 = frames_mode(R, sc, steps_x, args.warmup, "f32", tonemap, 0)
-            b32 = f32["px"] * (12 + (3 if tonemap >= 0 else 0))
-            a32 = b32 / (f32["region_ms"] / 1e3) / 1e9
+    res = split_frames(R, sc, args.steps, args.warmup, batch, args.hdr, tonemap, args.row_block,
+                       not args.no_pipeline, args.event_every)
+    elapsed = res["elapsed"]
+    value = res["rays"] * args.steps / elapsed / 1e6
+    summ = per_rank_summary(res)
+    r0 = res["ranks"][0]
+    # the trace kernel: rank 0's render per frame (HIP events around each timed batch launch)
+    render_ms = r0[0]
+    bytes_per_frame = int(r0[3]) * W * (HDR_BYTES[args.hdr] + 3)
+    achieved = bytes_per_frame / (render_ms / 1e3) / 1e9 if render_ms > 0 else 0.0
+    traffic, traffic_src = load_profile(f"pmc_{args.config}_frames.json")
+    valu, valu_src = load_profile(f"r04_{args.config}_valu.json")
+    if valu is None:
+        valu, valu_src = load_profile(f"r03_{args.config}_valu.json")
+    line = {
+        "metric": "Mrays/sec (primary+shadow) at 1920x1080" if args.config == "c2"
+                  else f"Mrays/sec (primary+shadow), config {args.config}",
+        "value": round(value, 3), "unit": "Mrays/s", "n_gpus": R.world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": workload_text(sc, R.world, args.row_block, batch, args.hdr,
+                                      args.tonemap),
+            "global_batch": args.steps, "resolution": [W, H],
+            "parallelism": f"block-cyclic rows ({args.row_block}-row blocks) x{R.world} + one "
+                           f"ncclGather per frame",
+            "frames_per_call": batch, "rays_per_frame": int(res["rays"]),
+        },
+        "frames_per_sec": round(args.steps / elapsed, 3),
+        "clock_warmup_ms": args.clock_warmup_ms,
+        "kernel_ms_per_frame": round(render_ms, 6),
+        "kernel_ms_per_launch": round(render_ms * batch, 6),
+        **summ,
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": (traffic.get("hbm_bytes_per_launch") if traffic and R.world == 1
+                        else None),
+            "alg_bytes_per_launch": bytes_per_frame * batch,
+            "alg_bytes_per_frame": bytes_per_frame,
+            "traffic_source": traffic_src if R.world == 1 else None,
+            "note": "rank 0's batch launch: its rows' framebuffer bytes (HDR + u8) per frame / "
+                    "its render time per frame (HIP events around every "
+                    f"{args.event_every}-th timed batch launch of {batch} frames)",
+        },
+        "valu": valu if R.world == 1 else None,
+        "valu_source": valu_src if R.world == 1 else None,
+        "cpu_baseline": None,
+    }
+    if extras:
+        steps_x = min(args.steps, 96)
+        # one launch per frame: the round-3 headline path
+        v1, ms1, k1 = single_launch_frames(R, sc, steps_x, args.warmup, tonemap)
+        (v1,) = R.sum_over_ranks(v1)
+        line["single_launch"] = {"value": round(v1, 3), "ms_per_frame": round(ms1, 5),
+                                 "kernel_ms_per_launch": round(k1, 6),
+                                 "note": "every rank its own whole frames, one launch each "
+                                         "(rt_render_device)"}
+        # weak scaling: every rank its own whole frames, batched
+        wk = split_frames(R, sc, steps_x, args.warmup, batch, args.hdr, tonemap, gather=False)
+        (rays_w,) = R.sum_over_ranks(float(wk["rays_rank"]))
+        line["weak_frames"] = {
+            "value": round(rays_w * steps_x / wk["elapsed"] / 1e6, 3),
+            "ms_per_step": round(wk["elapsed"] / steps_x * 1e3, 5), "scaling": "weak",
+            "workload": f"{sc.name} whole frames on every rank ({args.hdr} HDR + u8), "
+                        f"{batch} per call"}
+        if R.world == 1:
+            f32 = split_frames(R, sc, steps_x, args.warmup, batch, "f32", tonemap)
+            k32 = f32["ranks"][0][0]
+            b32 = res["px"] * 15
+            a32 = b32 / (k32 / 1e3) / 1e9 if k32 > 0 else 0.0
             line["roofline_f32"] = {
                 "achieved": round(a32, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(a32 / HBM_PEAK_GBS, 5), "alg_bytes_per_launch": b32,
-                "kernel_ms_per_launch": round(f32["region_ms"], 6),
+                "frac": round(a32 / HBM_PEAK_GBS, 5), "alg_bytes_per_frame": b32,
+                "kernel_ms_per_frame": round(k32, 6),
                 "value": round(f32["rays"] * steps_x / f32["elapsed"] / 1e6, 3)}
-            # a camera that moves every frame: never the cached per-camera packet image
-            mv = frames_mode(R, sc, steps_x, args.warmup, args.hdr, tonemap, 0,
-                             camera_step=lambda base, i: base + (i * 1e-7, 0.0, 0.0))
+            mv = split_frames(R, sc, steps_x, args.warmup, batch, args.hdr, tonemap,
+                              camera_step=lambda base, i: base + (i * 1e-7, 0.0, 0.0))
             line["moving_camera"] = {
                 "ms_per_step": round(mv["elapsed"] / steps_x * 1e3, 5),
-                "kernel_ms_per_launch": round(mv["region_ms"], 6),
+                "kernel_ms_per_frame": round(mv["ranks"][0][0], 6),
                 "value": round(mv["rays"] * steps_x / mv["elapsed"] / 1e6, 3),
-                "note": "camera x moved by 1e-7 every frame: the per-camera packet image is "
-                        "never reused (each launch's first workgroup forms it and hands it to "
-                        "the later ones, DESIGN §4); rays counted at the first position"}
-            if args.inflight > 1:
-                el = pipelined_frames(R, sc, steps_x, args.warmup, args.inflight, tonemap)
-                line["pipelined"] = {
-                    "inflight": args.inflight,
-                    "value": round(rays_rank * steps_x / el / 1e6, 3),
-                    "ms_per_step": round(el / steps_x * 1e3, 5),
-                    "note": "the same frames through the C-ABI serving queue (rt_queue), "
-                            "several in flight on separate HIP streams; serving throughput, "
-                            "not the headline value"}
-            # BASELINE config 1: the reference main()'s own scene and sampling
+                "note": "camera x moved by 1e-7 every frame: no frame reuses a cached per-camera "
+                        "packet image (each frame's first workgroup forms it and hands it to the "
+                        "later ones, DESIGN §4); rays counted at the first position"}
             sc1 = make_config("c1", aa=32)
-            c1 = frames_mode(R, sc1, 10, 2, "f64", R.capi.TONEMAPS.index("aces"), 0)
+            v, ms, k = single_launch_frames(R, sc1, 10, 2, capi.TONEMAPS.index("aces"))
             line["reference_main_c1"] = {
                 "workload": "c1: the reference main() box (5 mirrored axis planes, 2 point "
                             "lights), 1000x1000, AA=32, f64 Vec3 HDR + fused ACES u8",
-                "ms_per_frame": round(c1["elapsed"] / 10 * 1e3, 4),
-                "kernel_ms_per_launch": round(c1["region_ms"], 4),
-                "rays_per_frame": c1["rays"],
-                "value": round(c1["rays"] * 10 / c1["elapsed"] / 1e6, 3), "unit": "Mrays/s"}
+                "ms_per_frame": round(ms, 4), "kernel_ms_per_launch": round(k, 4),
+                "value": round(v, 3), "unit": "Mrays/s"}
             line["d2h"] = d2h_frames(R, sc, min(args.steps, 20), tonemap)
-            # the N>1 default workload (C4 tiled + RCCL gather) on this one GPU
-            sc4 = make_config("c4", aa=1)
-            t1 = tiled_mode(R, sc4, min(args.steps, 20), min(args.warmup, 3), "u8", 1,
-                            args.row_block, 1, not args.no_pipeline)
-            line["tiled_1gpu"] = tiled_summary(t1, min(args.steps, 20), sc4.camera.width, "u8",
-                                               args.row_block)
-            line["tiled_1gpu"]["workload"] = ("c4 7680x4320, 256 spheres, 8 lights, Reinhard "
-                                              "u8 through rt_render_gather on 1 rank")
-        if R.world == 1 and not args.no_cpu_baseline:
-            try:
-                line["cpu_baseline"] = cpu_baseline(sc, rays_rank, args.cpu_frames)
-            except Exception as e:  # a reported baseline, never the product path
-                line["cpu_baseline"] = {"error": repr(e)}
-    else:
-        res = tiled_mode(R, sc, args.steps, args.warmup, args.gather, tonemap, args.row_block,
-                         args.event_every, not args.no_pipeline)
-        summ = tiled_summary(res, args.steps, W, args.gather, args.row_block)
-        elapsed = res["elapsed"]
-        value = res["rays"] * args.steps / elapsed / 1e6
-        r0 = res["ranks"][0]
-        bytes_rank0 = int(r0[3]) * W * res["bpp"]
-        achieved = bytes_rank0 / (r0[0] / 1e3) / 1e9 if r0[0] > 0 else 0.0
-        line = {
-            "metric": "Mrays/sec (primary+shadow), row-tiled frame + RCCL gather",
-            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": R.world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic",
-            "config": {
-                "workload": f"{config}: {W}x{H}, {len(sc.spheres)} spheres, {len(sc.planes)} "
-                            f"planes, {len(sc.lights)} point lights, AA=1, one frame per step "
-                            f"split over {R.world} GPUs, fused {args.tonemap} {args.gather} "
-                            f"gathered to rank 0",
-                "global_batch": args.steps, "resolution": [W, H],
-                "parallelism": f"block-cyclic rows ({args.row_block}-row blocks) x{R.world} + "
-                               f"one ncclGather per frame",
-                "rays_per_frame": res["rays"],
-            },
-            "frames_per_sec": round(args.steps / elapsed, 3),
-            "clock_warmup_ms": args.clock_warmup_ms,
-            "tiled": summ,
-            "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "alg_bytes_per_launch": bytes_rank0,
-                "note": "rank 0's render launch: its rows' framebuffer bytes / render time",
-            },
-            "cpu_baseline": None,
-        }
-        if extras:
-            sc2 = make_config("c2", aa=1)
-            wk = frames_mode(R, sc2, args.steps, args.warmup, "f64", tonemap, 0)
-            (rays2,) = R.sum_over_ranks(float(wk["rays"]))
-            line["weak_frames"] = {
-                "value": round(rays2 * args.steps / wk["elapsed"] / 1e6, 3),
-                "ms_per_step": round(wk["elapsed"] / args.steps * 1e3, 5),
-                "workload": "c2 1920x1080 frames, every rank its own (f64 Vec3 + Reinhard u8)",
-                "scaling": "weak"}
+        # BASELINE config 4: the 8K frame row-tiled through the same path
+        sc4 = make_config("c4", aa=1)
+        t4 = split_frames(R, sc4, min(args.steps, 16), min(args.warmup, 2), 2, "f64", tonemap,
+                          args.row_block, not args.no_pipeline, 1)
+        line["c4_tiled"] = {
+            "value": round(t4["rays"] * min(args.steps, 16) / t4["elapsed"] / 1e6, 3),
+            "ms_per_frame": round(t4["elapsed"] / min(args.steps, 16) * 1e3, 5),
+            "workload": "c4 7680x4320, 256 spheres, 8 lights, f64 HDR rows on each rank + "
+                        "Reinhard u8 gathered, 2 frames per call",
+            **per_rank_summary(t4)}
+    if R.world == 1 and not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline(sc, res["rays_rank"], args.cpu_frames)
+        except Exception as e:  # a reported baseline, never the product path
+            line["cpu_baseline"] = {"error": repr(e)}
     if R.rank == 0:
         print(json.dumps(line), flush=True)
-    R.ctx.close()
-    if R.world > 1:
-        R.dist.destroy_process_group()
+    R.close()
 
 
 if __name__ == "__main__":

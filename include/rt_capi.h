@@ -278,6 +278,24 @@ rt_status rt_render_gather(rt_comm* comm, const rt_scene* scene, const rt_camera
 rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, int n,
                                const rt_camera* cam, const rt_render_opts* opts, int outputs,
                                void* d_hdr64, void* d_hdr32, void* d_ldr);
+/* A batch of nframes frames (see rt_render_batch: one camera per frame, same width / height /
+ * focal / aa_samples) in one call: this rank renders its rows of every frame in one launch,
+ * then ONE ncclGather per frame and gathered output — all of them in one ncclGroup, so a batch
+ * costs one RCCL launch — and rank 0 assembles every frame (one launch).  On rank 0 the d_* hold
+ * nframes whole frames back to back (frame f at f*W*H*3 elements).  rank_* (any may be NULL)
+ * receive outputs that are rendered but NOT gathered: this rank's rows of every frame, packed
+ * (frame f at f*rows*W*3, rows = rt_gather_timing.rows) — e.g. the float64 HDR framebuffer
+ * kept where it was rendered while the tonemapped bytes are gathered.  An output is either
+ * gathered (in `outputs`) or rank-local, not both.  rt_render_gather = nframes 1, no rank_*. */
+rt_status rt_render_gather_batch(rt_comm* comm, const rt_scene* scene, const rt_camera* cams,
+                                 int nframes, const rt_render_opts* opts, int outputs,
+                                 void* d_hdr64, void* d_hdr32, void* d_ldr, void* rank_hdr64,
+                                 void* rank_hdr32, void* rank_ldr);
+/* rt_render_gather_all for a batch of frames (the layouts of rt_render_gather_batch). */
+rt_status rt_render_gather_all_batch(rt_comm* const* comms, rt_scene* const* scenes, int n,
+                                     const rt_camera* cams, int nframes,
+                                     const rt_render_opts* opts, int outputs, void* d_hdr64,
+                                     void* d_hdr32, void* d_ldr);
 /* Waits for every frame enqueued on the communicator (render, gather, assembly). */
 rt_status rt_comm_synchronize(rt_comm* comm);
 /* Summed frame timings since the last reset (waits for the timed frames to finish). */
@@ -288,6 +306,16 @@ rt_status rt_comm_timing(rt_comm* comm, rt_gather_timing* out, int reset);
 rt_status rt_render_device(rt_context* ctx, const rt_scene* scene, const rt_camera* cam,
                            const rt_render_opts* opts, void* d_hdr64, void* d_hdr32,
                            void* d_ldr);
+/* A batch of frames: Scene::RenderImage (Scene.h:311-328) once per camera of cams[0..nframes)
+ * — views of one scene from several positions (an animation's frames, a camera path) — into
+ * device buffers holding the frames back to back (frame f at f*rows*W*3 elements of each
+ * output).  Every camera must have cams[0]'s width, height, focal and aa_samples; the position
+ * may differ.  Scenes the packet kernel renders (no secondary rays) take up to 16 frames per
+ * launch (one grid plane per frame), so the launch's ramp and drain are paid once per batch;
+ * other scenes take one launch per frame.  Each frame is the frame rt_render_device gives. */
+rt_status rt_render_batch(rt_context* ctx, const rt_scene* scene, const rt_camera* cams,
+                          int nframes, const rt_render_opts* opts, void* d_hdr64,
+                          void* d_hdr32, void* d_ldr);
 
 /* ---- Serving frame queue -------------------------------------------------------------------
  * Consecutive Scene::RenderImage() frames (Scene.h:311-328) into device framebuffers with

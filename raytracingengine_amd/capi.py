@@ -45,7 +45,8 @@ EXPORTED = [
     "rt_comm_timing", "rt_comm_synchronize", "rt_debug_assemble_rows", "rt_debug_tile_order",
     "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
     "rt_debug_f64_ops", "rt_debug_vec_ops", "rt_queue_create", "rt_queue_destroy",
-    "rt_queue_submit", "rt_queue_wait", "rt_queue_synchronize",
+    "rt_queue_submit", "rt_queue_wait", "rt_queue_synchronize", "rt_render_batch",
+    "rt_render_gather_batch", "rt_render_gather_all_batch",
 ]
 
 
@@ -122,6 +123,7 @@ def load_library(path: str = LIB_PATH):
         "rt_scene_set_area_light": [vp, vp],
         "rt_render": [vp, vp, vp, vp, vp, vp, vp, vp],
         "rt_render_device": [vp, vp, vp, vp, vp, vp, vp],
+        "rt_render_batch": [vp, vp, vp, i32, vp, vp, vp, vp],
         "rt_render_multi": [vp, vp, i32, vp, vp, vp, vp, vp, vp],
         "rt_stats_read": [vp, vp],
         "rt_stats_reset": [vp],
@@ -138,6 +140,8 @@ def load_library(path: str = LIB_PATH):
         "rt_comm_info": [vp, vp, vp],
         "rt_render_gather": [vp, vp, vp, vp, i32, vp, vp, vp],
         "rt_render_gather_all": [vp, vp, i32, vp, vp, i32, vp, vp, vp],
+        "rt_render_gather_batch": [vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp],
+        "rt_render_gather_all_batch": [vp, vp, i32, vp, i32, vp, i32, vp, vp, vp],
         "rt_comm_timing": [vp, vp, i32],
         "rt_comm_synchronize": [vp],
         "rt_queue_create": [vp, i32, vp],
@@ -380,6 +384,21 @@ class DeviceScene:
         _check(_lib.rt_render_device(self.ctx.handle, self._h, self.camera.ctypes.data,
                                      ctypes.byref(opts), d_hdr64, d_hdr32, d_ldr))
 
+    def cameras(self, positions) -> np.ndarray:
+        """rt_camera records of this scene's camera moved to each of `positions` ([n, 3])."""
+        pos = np.asarray(positions, np.float64).reshape(-1, 3)
+        cams = np.repeat(self.camera, len(pos))
+        cams["position"] = pos
+        return cams
+
+    def render_batch(self, cams: np.ndarray, d_hdr64: int | None, d_hdr32: int | None,
+                     d_ldr: int | None, opts: RenderOpts):
+        """Asynchronous render of len(cams) frames into device buffers holding them back to
+        back (rt_render_batch)."""
+        cams = np.ascontiguousarray(cams)
+        _check(_lib.rt_render_batch(self.ctx.handle, self._h, cams.ctypes.data, len(cams),
+                                    ctypes.byref(opts), d_hdr64, d_hdr32, d_ldr))
+
 
 def render_multi(scenes: list, *, hdr64=True, tonemap: int = TONEMAP_NONE, stats=False,
                  row_block: int = 0, **opt_kw) -> dict:
@@ -498,6 +517,18 @@ class Comm:
         _check(_lib.rt_render_gather(self._h, dscene._h, dscene.camera.ctypes.data,
                                      ctypes.byref(opts), outputs, d_hdr64, d_hdr32, d_ldr))
 
+    def render_gather_batch(self, dscene: "DeviceScene", cams: np.ndarray, opts: RenderOpts,
+                            outputs: int, d_hdr64: int | None = None, d_hdr32: int | None = None,
+                            d_ldr: int | None = None, rank_hdr64: int | None = None,
+                            rank_hdr32: int | None = None, rank_ldr: int | None = None):
+        """Collective: len(cams) frames, this rank's rows of each in one launch, one gather per
+        frame and output in one RCCL group, rank 0 assembles (rt_render_gather_batch);
+        rank_* receive outputs rendered but not gathered (this rank's rows)."""
+        cams = np.ascontiguousarray(cams)
+        _check(_lib.rt_render_gather_batch(self._h, dscene._h, cams.ctypes.data, len(cams),
+                                           ctypes.byref(opts), outputs, d_hdr64, d_hdr32, d_ldr,
+                                           rank_hdr64, rank_hdr32, rank_ldr))
+
     def synchronize(self):
         _check(_lib.rt_comm_synchronize(self._h))
 
@@ -551,3 +582,17 @@ def render_gather_all(comms: list, scenes: list, opts: RenderOpts, outputs: int,
     _check(load_library().rt_render_gather_all(cs, ss, n, scenes[0].camera.ctypes.data,
                                                ctypes.byref(opts), outputs, d_hdr64, d_hdr32,
                                                d_ldr))
+
+
+def render_gather_all_batch(comms: list, scenes: list, cams: np.ndarray, opts: RenderOpts,
+                            outputs: int, d_hdr64: int | None = None, d_hdr32: int | None = None,
+                            d_ldr: int | None = None):
+    """rt_render_gather_all_batch: a batch of frames over every rank of a Comm.create_all /
+    create_local group from this process."""
+    n = len(comms)
+    cs = (ctypes.c_void_p * n)(*[c.handle for c in comms])
+    ss = (ctypes.c_void_p * n)(*[s._h for s in scenes])
+    cams = np.ascontiguousarray(cams)
+    _check(load_library().rt_render_gather_all_batch(cs, ss, n, cams.ctypes.data, len(cams),
+                                                     ctypes.byref(opts), outputs, d_hdr64,
+                                                     d_hdr32, d_ldr))

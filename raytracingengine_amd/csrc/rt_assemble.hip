@@ -28,6 +28,9 @@ __global__ __launch_bounds__(256) void assemble_rows_kernel(const V* __restrict_
                                                             uint32_t words_per_row,
                                                             uint32_t height, uint32_t block,
                                                             uint32_t n, uint32_t max_rows) {
+    // frame blockIdx.z of a batch: n·max_rows gathered rows in, height image rows out
+    src += static_cast<size_t>(blockIdx.z) * n * max_rows * words_per_row;
+    dst += static_cast<size_t>(blockIdx.z) * height * words_per_row;
     // one workgroup row-strip: blockIdx.y walks image rows, x covers the row's words
     for (uint32_t y = blockIdx.y; y < height; y += gridDim.y) {
         const V* s = src + gathered_row(y, block, n, max_rows) * words_per_row;
@@ -40,12 +43,13 @@ __global__ __launch_bounds__(256) void assemble_rows_kernel(const V* __restrict_
 
 template <typename V>
 hipError_t launch_as(const void* src, void* dst, size_t row_bytes, uint32_t height,
-                     uint32_t block, uint32_t n, uint32_t max_rows, hipStream_t stream) {
+                     uint32_t block, uint32_t n, uint32_t max_rows, uint32_t frames,
+                     hipStream_t stream) {
     const uint32_t words = static_cast<uint32_t>(row_bytes / sizeof(V));
     const uint32_t gx = (words + 255) / 256;
     // enough rows in flight to fill 256 CUs several times over; rows loop inside
     const uint32_t gy = height < 4096u ? height : 4096u;
-    hipLaunchKernelGGL(assemble_rows_kernel<V>, dim3(gx, gy), dim3(256), 0, stream,
+    hipLaunchKernelGGL(assemble_rows_kernel<V>, dim3(gx, gy, frames), dim3(256), 0, stream,
                        static_cast<const V*>(src), static_cast<V*>(dst), words, height, block,
                        n, max_rows);
     return hipGetLastError();
@@ -55,16 +59,19 @@ hipError_t launch_as(const void* src, void* dst, size_t row_bytes, uint32_t heig
 
 hipError_t launch_assemble_rows(const void* gathered, void* image, size_t row_bytes,
                                 uint32_t height, uint32_t block, uint32_t n, uint32_t max_rows,
-                                hipStream_t stream) {
-    if (height == 0 || row_bytes == 0) return hipSuccess;
+                                uint32_t frames, hipStream_t stream) {
+    if (height == 0 || row_bytes == 0 || frames == 0) return hipSuccess;
     const uintptr_t align = reinterpret_cast<uintptr_t>(gathered) |
                             reinterpret_cast<uintptr_t>(image) | row_bytes |
                             static_cast<uintptr_t>(max_rows * row_bytes);
     if (align % 16 == 0)
-        return launch_as<uint4>(gathered, image, row_bytes, height, block, n, max_rows, stream);
+        return launch_as<uint4>(gathered, image, row_bytes, height, block, n, max_rows, frames,
+                                  stream);
     if (align % 4 == 0)
-        return launch_as<uint32_t>(gathered, image, row_bytes, height, block, n, max_rows, stream);
-    return launch_as<uint8_t>(gathered, image, row_bytes, height, block, n, max_rows, stream);
+        return launch_as<uint32_t>(gathered, image, row_bytes, height, block, n, max_rows, frames,
+                                  stream);
+    return launch_as<uint8_t>(gathered, image, row_bytes, height, block, n, max_rows, frames,
+                                  stream);
 }
 
 }  // namespace rtamd

@@ -211,6 +211,8 @@ rt_status build_params(rt_context* ctx, const rt_scene* sc, const rt_camera* cam
 // positions are remembered.  Past kMaxPkImages cached cameras the kernel forms it in LDS.
 constexpr size_t kMaxPkImages = 16;
 constexpr size_t kMaxPkSeen = 16;
+// Launch shapes (grid, row set) with their own costliest-first tile order per cached camera.
+constexpr size_t kMaxTileOrders = 8;
 // A camera without a cached image gets a publish slot instead: the launch's first workgroup
 // forms the image and hands it to the later ones through {epoch, word} granules (rt_packet.hip).
 // Slots rotate so that launches in flight on other streams keep theirs; a slot overwritten by a
@@ -218,7 +220,7 @@ constexpr size_t kMaxPkSeen = 16;
 // kPkPubMaxWords 32-bit words (4 KiB, about 32 spheres) are formed per workgroup: reading twice
 // their size in granules costs as much as forming them (moving camera, MI355X: C2's 1.9 KiB
 // image 54.1 -> 50.8 us; C3's 14.3 KiB 555 -> 555 us; C5's 6.5 KiB 522 -> 530 us).
-constexpr size_t kPkPubSlots = 8;
+constexpr size_t kPkPubSlots = 32;
 constexpr size_t kPkPubMaxWords = 1024;
 // Epochs are unique across the process (not per scene): a slot whose memory held another
 // scene's granules (a freed and re-allocated buffer) can never match a later launch's tags.
@@ -264,21 +266,35 @@ rt_status tile_order(rt_context* ctx, rt_scene::PkImage& im, TraceParams& p, int
                      rt_scene::PkImage::TileOrder** rec) {
     *rec = nullptr;
     if (flags & RT_FLAG_NO_TILE_ORDER) return RT_OK;
-    auto& o = im.ord;
     uint32_t gx, gy, waves;
     packet_grid(p, gx, gy, waves);
     const uint32_t key[8] = {gx, gy, waves, p.width, p.height, p.rows, p.row0,
                              (p.row_block << 16) ^ p.row_stride};
     const uint32_t tiles = gx * gy;
-    if (o.state == 0 || std::memcmp(o.key, key, sizeof key) != 0) {  // record this launch
-        RT_HIP(o.cost.ensure(sizeof(uint32_t) * tiles * waves));
-        if (!o.recorded) RT_HIP(hipEventCreateWithFlags(&o.recorded, hipEventDisableTiming));
+    size_t idx = 0;
+    while (idx < im.ords.size() && std::memcmp(im.ords[idx].key, key, sizeof key) != 0) ++idx;
+    if (idx == im.ords.size()) {  // a new launch shape: record this launch
+        if (im.ords.size() >= kMaxTileOrders) return RT_OK;  // the default order
+        if (im.ords.capacity() < kMaxTileOrders) im.ords.reserve(kMaxTileOrders);
+        im.ords.emplace_back();
+        auto& o = im.ords.back();
+        im.last_ord = static_cast<int>(idx);
+        hipError_t e = o.cost.ensure(sizeof(uint32_t) * tiles * waves);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&o.recorded, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            o.cost.release();
+            im.ords.pop_back();
+            im.last_ord = -1;
+            return hip_fail(e, "tile order");
+        }
         std::memcpy(o.key, key, sizeof key);
         o.state = 1;
         p.tile_cost = static_cast<uint32_t*>(o.cost.ptr);
         *rec = &o;
         return RT_OK;
     }
+    auto& o = im.ords[idx];
+    im.last_ord = static_cast<int>(idx);
     if (o.state == 1) {  // build the order (after the recording launch, on whatever stream)
         RT_HIP(o.keys.ensure(sizeof(uint32_t) * tiles));
         RT_HIP(o.order.ensure(sizeof(uint32_t) * tiles));
@@ -326,6 +342,8 @@ rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p, int 
     }
     if (sc->pk_images.size() >= kMaxPkImages) return packet_publish_slot(ctx, sc, p);
     seen.erase(it);
+    // never reallocated: a frame batch holds entries of earlier frames while adding one
+    if (sc->pk_images.capacity() < kMaxPkImages) sc->pk_images.reserve(kMaxPkImages);
     sc->pk_images.emplace_back();
     rt_scene::PkImage& im = sc->pk_images.back();
     std::memcpy(im.cam, p.cam_pos, sizeof im.cam);
@@ -353,6 +371,17 @@ bool uses_wavefront_arena(int path, int flags) {
     return path == kPathTree || (path == kPathChain && wf_chain && std::atoi(wf_chain) == 1);
 }
 
+rt_status scratch_wait(rt_context* ctx) {
+    if (ctx->scratch_used) RT_HIP(hipStreamWaitEvent(ctx->stream, ctx->scratch_event, 0));
+    return RT_OK;
+}
+
+rt_status scratch_done(rt_context* ctx) {
+    RT_HIP(hipEventRecord(ctx->scratch_event, ctx->stream));
+    ctx->scratch_used = true;
+    return RT_OK;
+}
+
 bool render_uses_context_scratch(const rt_scene* sc, const rt_render_opts* opts) {
     rt_render_opts o;
     if (opts) o = *opts;
@@ -364,14 +393,35 @@ bool render_uses_context_scratch(const rt_scene* sc, const rt_render_opts* opts)
     return uses_wavefront_arena(path, o.flags);
 }
 
+rt_status check_batch(const rt_camera* cams, int nframes) {
+    if (!cams || nframes < 1) return fail(RT_ERR_INVALID_ARG, "frame batch: no cameras");
+    for (int f = 0; f < nframes; ++f) {
+        rt_status st = validate_camera(cams + f);
+        if (st != RT_OK) return st;
+        if (cams[f].width != cams[0].width || cams[f].height != cams[0].height ||
+            cams[f].aa_samples != cams[0].aa_samples ||
+            std::memcmp(&cams[f].focal, &cams[0].focal, sizeof(double)) != 0)
+            return fail(RT_ERR_INVALID_ARG, "frame batch: every camera must have the first's "
+                                            "width, height, focal and aa_samples");
+    }
+    return RT_OK;
+}
+
 rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
+                         const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr) {
+    return enqueue_frames(ctx, sc, cam, 1, opts, d64, d32, dldr);
+}
+
+rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* cams, int nframes,
                          const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr) {
     TraceParams p;
     int path;
     bool lds;
     size_t lds_bytes;
     uint32_t rows;
-    rt_status st = build_params(ctx, sc, cam, opts, p, path, lds, lds_bytes, rows);
+    rt_status st = nframes == 1 ? RT_OK : check_batch(cams, nframes);
+    if (st != RT_OK) return st;
+    st = build_params(ctx, sc, cams, opts, p, path, lds, lds_bytes, rows);
     if (st != RT_OK) return st;
     p.out64 = d64;
     p.out32 = d32;
@@ -379,6 +429,27 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
     const int flags = opts ? opts->flags : 0;
     if (!dldr) p.tonemap = RT_TONEMAP_NONE;
     if (dldr && p.tonemap == RT_TONEMAP_NONE) p.ldr = nullptr;
+    const bool packet_path = path == kPathDirect && !(flags & RT_FLAG_GENERIC_KERNEL) &&
+                             p.ns <= packet_max_spheres() &&
+                             packet_lds_bytes(p.ns, p.np, p.nl) <= ctx->lds_limit;
+    const size_t frame_px = static_cast<size_t>(rows) * p.width;
+    if (nframes > 1 && (!packet_path || nframes > kPkMaxBatch)) {
+        // one launch per frame (other kernels), or per kPkMaxBatch frames
+        const int step = packet_path ? kPkMaxBatch : 1;
+        for (int f0 = 0; f0 < nframes; f0 += step) {
+            const size_t off = 3 * frame_px * static_cast<size_t>(f0);
+            st = enqueue_frames(ctx, sc, cams + f0, std::min(step, nframes - f0), opts,
+                                d64 ? d64 + off : nullptr, d32 ? d32 + off : nullptr,
+                                dldr ? dldr + off : nullptr);
+            if (st != RT_OK) return st;
+        }
+        return RT_OK;
+    }
+    const bool scratch = (flags & RT_FLAG_COUNT_RAYS) || uses_wavefront_arena(path, flags);
+    if (scratch) {
+        st = scratch_wait(ctx);
+        if (st != RT_OK) return st;
+    }
 
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (flags & RT_FLAG_TIME_KERNEL) {
@@ -396,13 +467,35 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
         RT_HIP(hipEventRecord(ev.first, ctx->stream));
     }
     // Scenes without secondary rays take the packet-culled kernel when its LDS image fits.
-    const bool packet = path == kPathDirect && !(flags & RT_FLAG_GENERIC_KERNEL) &&
-                        p.ns <= packet_max_spheres() &&
-                        packet_lds_bytes(p.ns, p.np, p.nl) <= ctx->lds_limit;
+    const bool packet = packet_path;
     rt_scene::PkImage::TileOrder* rec = nullptr;  // set: this launch records wave durations
     if (packet) {
         st = packet_image(ctx, sc, p, flags, &rec);
         if (st != RT_OK) return st;
+    }
+    if (packet && nframes > 1) {
+        // a frame batch: frame f's camera and image source (cached image, hand-off slot, or
+        // formed per workgroup); the tile order is the first frame's (it permutes tiles only)
+        p.nframes = static_cast<uint32_t>(nframes);
+        p.frame_px = frame_px;
+        for (int f = 0; f < nframes; ++f) {
+            TraceParams q = p;
+            if (f > 0) {
+                q.pk_image = nullptr;
+                q.pk_pub = nullptr;
+                q.pk_epoch = 0;
+                for (int i = 0; i < 3; ++i) q.cam_pos[i] = cams[f].position[i];
+                rt_scene::PkImage::TileOrder* unused = nullptr;
+                st = packet_image(ctx, sc, q, flags | RT_FLAG_NO_TILE_ORDER, &unused);
+                if (st != RT_OK) return st;
+            }
+            PkFrame& F = p.fr[f];
+            for (int i = 0; i < 3; ++i) F.cam[i] = q.cam_pos[i];
+            F.img = q.pk_image;
+            F.pub = q.pk_pub;
+            F.epoch = q.pk_epoch;
+            F._pad = 0;
+        }
     }
     // generic kernels without triangle / area-light code for scenes that use neither
     const bool lean_generic = p.nt == 0 && p.al_samples == 0;
@@ -459,7 +552,7 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
         pc.tile_cost = nullptr;  // the durations are the image launch's
         RT_HIP(launch(pc, true));
     }
-    return RT_OK;
+    return scratch ? scratch_done(ctx) : RT_OK;
 }
 
 }  // namespace rtamd
@@ -506,6 +599,7 @@ rt_status rt_context_create(int device, rt_context** out) {
     hipError_t e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = ctx->counters.ensure(2 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(ctx->counters.ptr, 0, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->scratch_event, hipEventDisableTiming);
     if (e != hipSuccess) {
         rt_context_destroy(ctx);
         return hip_fail(e, "rt_context_create");
@@ -524,6 +618,10 @@ rt_status rt_context_destroy(rt_context* ctx) {
             (void)hipEventDestroy(ev.first);
             (void)hipEventDestroy(ev.second);
         }
+    if (ctx->scratch_event) {
+        (void)hipEventSynchronize(ctx->scratch_event);
+        (void)hipEventDestroy(ctx->scratch_event);
+    }
     leave_groups(ctx);  // communicators of any group this context is in go first
     for (DeviceBuffer* b : {&ctx->out64, &ctx->out32, &ctx->ldr, &ctx->tm_in, &ctx->tm_out,
                             &ctx->dbg, &ctx->rays, &ctx->counters, &ctx->wf, &ctx->wf_ctl})
@@ -732,12 +830,14 @@ rt_status rt_scene_destroy(rt_scene* sc) {
     for (auto& im : sc->pk_images) {
         im.buf.release();
         if (im.ready) (void)hipEventDestroy(im.ready);
-        im.ord.cost.release();
-        im.ord.keys.release();
-        im.ord.order.release();
-        if (im.ord.recorded) (void)hipEventDestroy(im.ord.recorded);
-        if (im.ord.built) (void)hipEventDestroy(im.ord.built);
-        if (im.ord.verdict) (void)hipHostFree(im.ord.verdict);
+        for (auto& o : im.ords) {
+            o.cost.release();
+            o.keys.release();
+            o.order.release();
+            if (o.recorded) (void)hipEventDestroy(o.recorded);
+            if (o.built) (void)hipEventDestroy(o.built);
+            if (o.verdict) (void)hipHostFree(o.verdict);
+        }
     }
     delete sc;
     return RT_OK;
@@ -766,6 +866,17 @@ rt_status rt_render_device(rt_context* ctx, const rt_scene* sc, const rt_camera*
                    static_cast<uint8_t*>(dldr));
 }
 
+rt_status rt_render_batch(rt_context* ctx, const rt_scene* sc, const rt_camera* cams,
+                          int nframes, const rt_render_opts* opts, void* d64, void* d32,
+                          void* dldr) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARG, "context is NULL");
+    rt_status st = check_batch(cams, nframes);
+    if (st != RT_OK) return st;
+    DeviceGuard g(ctx->device);
+    return enqueue_frames(ctx, sc, cams, nframes, opts, static_cast<double*>(d64),
+                          static_cast<float*>(d32), static_cast<uint8_t*>(dldr));
+}
+
 rt_status rt_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
                     const rt_render_opts* opts, double* h64, float* h32, uint8_t* hldr,
                     rt_stats* stats) {
@@ -783,6 +894,8 @@ rt_status rt_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
     if (h32) RT_HIP(ctx->out32.ensure(npx * 3 * sizeof(float)));
     if (hldr) RT_HIP(ctx->ldr.ensure(npx * 3));
     if (stats) {
+        st = scratch_wait(ctx);  // the counters: after any counting render on another stream
+        if (st != RT_OK) return st;
         RT_HIP(hipMemsetAsync(ctx->counters.ptr, 0, 2 * sizeof(unsigned long long), ctx->stream));
     }
     st = enqueue_render(ctx, sc, cam, &o, h64 ? static_cast<double*>(ctx->out64.ptr) : nullptr,
@@ -878,6 +991,8 @@ rt_status rt_trace_rays(rt_context* ctx, const rt_scene* sc, const rt_render_opt
     RT_HIP(hipMemcpyAsync(rgb, d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     if (stats) {
         p.counters = static_cast<unsigned long long*>(ctx->counters.ptr);
+        st = scratch_wait(ctx);
+        if (st != RT_OK) return st;
         RT_HIP(hipMemsetAsync(p.counters, 0, 2 * sizeof(unsigned long long), ctx->stream));
         RT_HIP(launch_trace_rays(p, path, true, d_rays, n, d_out, ctx->stream));
         unsigned long long c[2] = {0, 0};
@@ -961,7 +1076,8 @@ rt_status rt_debug_tile_order(rt_context* ctx, const rt_scene* sc, const rt_came
     RT_HIP(hipDeviceSynchronize());
     for (const auto& im : sc->pk_images) {
         if (std::memcmp(im.cam, cam->position, sizeof im.cam) != 0) continue;
-        const auto& o = im.ord;
+        if (im.last_ord < 0) return RT_OK;
+        const auto& o = im.ords[static_cast<size_t>(im.last_ord)];
         *state = o.state;
         if (o.state == 0) return RT_OK;
         *tiles = o.key[0] * o.key[1];

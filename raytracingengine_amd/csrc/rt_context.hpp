@@ -67,6 +67,10 @@ struct rt_context {
     rtamd::DeviceBuffer out64, out32, ldr, tm_in, tm_out, dbg, rays;
     rtamd::DeviceBuffer counters;  // 2 x u64
     rtamd::DeviceBuffer wf, wf_ctl;  // breadth-first TraceRay arena + its control block
+    // The arena and the counters are one per context: a render that uses them waits for the
+    // previous one that did, on whatever stream it ran (scratch_wait / scratch_done).
+    hipEvent_t scratch_event = nullptr;
+    bool scratch_used = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
     double timed_ms = 0.0;
@@ -107,7 +111,9 @@ struct rt_scene {
         bool done = false;
         // Costliest-first tile order of the packet kernel for this camera (rt_capi.cpp
         // tile_order): the wave durations one launch records, then the order built from them,
-        // for launches of the same shape (grid, rows) — state 0 none, 1 recorded, 2 ordered.
+        // for launches of the same shape (grid, rows) — state 1 recorded, 2 ordered.  One entry
+        // per launch shape (up to kMaxTileOrders), each written once and never rewritten, so a
+        // launch of one shape in flight on any stream never sees another shape's table.
         struct TileOrder {
             uint32_t key[8] = {};  // gx gy waves width height rows row0 row_block|row_stride
             int state = 0;
@@ -116,7 +122,9 @@ struct rt_scene {
             // pinned host word the order kernel fills: 0 not yet, 1 narrow (keep the default
             // order, no table), 2 dispatch by the table
             uint32_t* verdict = nullptr;
-        } ord;
+        };
+        std::vector<TileOrder> ords;
+        int last_ord = -1;  // the entry of the latest launch (rt_debug_tile_order)
     };
     mutable std::vector<PkImage> pk_images;
     mutable std::vector<std::array<double, 3>> pk_seen;  // cameras rendered once, no image yet
@@ -135,10 +143,20 @@ rt_status validate_camera(const rt_camera* cam);
 // device outputs in the packed row order of opts.  The caller holds a DeviceGuard.
 rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
                          const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr);
+// The same for a batch of nframes cameras (same width / height / focal / aa_samples): frame f
+// writes its rows f·rows·width pixels into each output.  Packet-kernel scenes render up to
+// kPkMaxBatch frames per launch (blockIdx.z = frame), other scenes one launch per frame.
+rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* cams, int nframes,
+                         const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr);
+rt_status check_batch(const rt_camera* cams, int nframes);
 // Whether a render uses scratch the context holds once (the breadth-first TraceRay arena, the
 // ray counters): frames on different streams that do must not overlap (rt_queue.cpp).
 bool uses_wavefront_arena(int path, int flags);
 bool render_uses_context_scratch(const rt_scene* sc, const rt_render_opts* opts);
+// Orders work on ctx->stream after the last render that used the context's scratch (any
+// stream), and marks ctx->stream's work so far as the latest such user.
+rt_status scratch_wait(rt_context* ctx);
+rt_status scratch_done(rt_context* ctx);
 // Adds the elapsed time of completed RT_FLAG_TIME_KERNEL event pairs to the context totals.
 rt_status harvest_events(rt_context* ctx, bool all);
 // rt_multi.cpp: releases the communicators rt_render_multi cached in ctx.

@@ -38,6 +38,17 @@ enum PathKind : int {
     kPathTree = 2     // some transparency > 0: refraction + reflection binary tree
 };
 
+// Packet kernel frame batches (rt_render_batch): frames of one scene and launch shape, one per
+// blockIdx.z, each with its own camera position and the camera-dependent packet-image source.
+constexpr int kPkMaxBatch = 16;
+struct PkFrame {
+    double cam[3];
+    const double* img;         // cached LDS image of this camera, or null
+    unsigned long long* pub;   // else: the in-launch hand-off slot, or null (form per workgroup)
+    uint32_t epoch;
+    uint32_t _pad;
+};
+
 struct TraceParams {
     // scene (device pointers into the scene allocation)
     const double* sph;
@@ -96,6 +107,12 @@ struct TraceParams {
     // normal ±e_x, ±e_y, ±e_z, any other
     const double* box;
     int32_t box_n[4];
+    // packet kernel frame batch: nframes > 0 replaces cam_pos / pk_image / pk_pub / pk_epoch
+    // by fr[blockIdx.z]; frame z writes its outputs frame_px pixels after frame z - 1's
+    uint32_t nframes;
+    uint32_t _pad2;
+    uint64_t frame_px;
+    PkFrame fr[kPkMaxBatch];
 };
 
 // Host: the spatial sphere chunks of the packet kernel's culls (rt_bvh.cpp): perm[sorted] =

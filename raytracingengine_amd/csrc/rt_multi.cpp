@@ -24,7 +24,7 @@ using namespace rtamd;
 namespace rtamd {
 hipError_t launch_assemble_rows(const void* gathered, void* image, size_t row_bytes,
                                 uint32_t height, uint32_t block, uint32_t n, uint32_t max_rows,
-                                hipStream_t stream);
+                                uint32_t frames, hipStream_t stream);
 }
 
 static_assert(RT_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "rt_capi.h id size");
@@ -48,10 +48,16 @@ struct rt_comm {
     hipStream_t gstream = nullptr;
     hipEvent_t rendered[2] = {nullptr, nullptr}, freed[2] = {nullptr, nullptr};
     bool slot_used[2] = {false, false};
+    // after this rank's latest frame (render, gather, assembly): what rt_comm_destroy waits for
+    hipEvent_t done = nullptr;
+    bool any_frame = false;
     uint64_t frame = 0;
     // RT_FLAG_TIME_KERNEL frames: before / after the render (context stream), before / after
     // the gather and after the assembly (gather stream)
-    struct Ev { hipEvent_t e[5]; };
+    struct Ev {
+        hipEvent_t e[5];
+        int frames = 1;  // frames of the batch these events bracket
+    };
     std::vector<Ev> pending, spare;
     double render_ms = 0, gather_ms = 0, assemble_ms = 0;
     uint64_t frames = 0;
@@ -124,7 +130,7 @@ rt_status harvest(rt_comm* c, bool all) {
         c->render_ms += a;
         c->gather_ms += b;
         c->assemble_ms += d;
-        c->frames += 1;
+        c->frames += static_cast<uint64_t>(ev.frames);
         c->spare.push_back(ev);
         ++done;
     }
@@ -132,15 +138,25 @@ rt_status harvest(rt_comm* c, bool all) {
     return RT_OK;
 }
 
-// One frame's state on one rank between the phases.
+// One frame batch's state on one rank between the phases (nframes frames of one plan).
 struct Frame {
     Plan pl;
     rt_comm::Ev* ev = nullptr;
     int slot = 0;
+    int nframes = 1;
     bool pipelined = false;
     bool direct = false;       // one rank: rendered into the framebuffers, nothing to gather
     hipStream_t gs = nullptr;  // the stream of the gather and the assembly
 };
+
+// Send buffer bytes per output kind k: frame f's packed rows start at f·rows (the render's own
+// frame stride) and every frame's gather sends max_rows rows from there, so the buffer holds
+// (nframes − 1)·rows + max_rows rows (the rows past a frame's own are the next frame's, or
+// padding: the assembly never reads them).
+size_t send_bytes(const Plan& pl, uint32_t width, int nframes, int k) {
+    const size_t rows = static_cast<size_t>(nframes - 1) * pl.rows + pl.max_rows;
+    return rows * width * bytes_per_px(k);
+}
 
 rt_status record(rt_comm::Ev* ev, int k, hipStream_t s) {
     if (!ev) return RT_OK;
@@ -148,25 +164,29 @@ rt_status record(rt_comm::Ev* ev, int k, hipStream_t s) {
     return RT_OK;
 }
 
-// Phase 1 of a frame on one rank: this rank's rows rendered into its send buffers.
-rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
-                      const rt_render_opts* opts, int outputs, void* const* dst, Frame& f) {
+// Phase 1 of a frame batch on one rank: this rank's rows rendered into its send buffers (the
+// gathered outputs) and into the caller's rank-local buffers (`local`, outputs not gathered).
+rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cams, int nframes,
+                      const rt_render_opts* opts, int outputs, void* const* dst,
+                      void* const* local, Frame& f) {
     rt_context* ctx = c->ctx;
     if (sc->ctx != ctx)
         return fail(RT_ERR_INVALID_ARG, "scene does not belong to the communicator's context");
+    const rt_camera* cam = cams;
     rt_status st = make_plan(cam, opts, c->nranks, c->rank, f.pl);
     if (st != RT_OK) return st;
     Plan& pl = f.pl;
+    f.nframes = nframes;
     // one rank: its rows are the whole frame in image order, rendered straight into the
     // caller's framebuffers (no send buffer, no gather, no assembly)
     f.direct = c->nranks == 1;
     f.pipelined = !f.direct && (pl.opts.flags & RT_FLAG_PIPELINE) != 0;
     f.slot = f.pipelined ? static_cast<int>(c->frame & 1) : 0;
     f.gs = f.pipelined ? c->gstream : ctx->stream;
-    const size_t npx = static_cast<size_t>(pl.max_rows) * cam->width;
+    const size_t npx = static_cast<size_t>(pl.max_rows) * cam->width * nframes;
     for (int k = 0; k < 3 && !f.direct; ++k) {
         if (!(outputs & kOutputs[k])) continue;
-        RT_HIP(c->send[f.slot][k].ensure(npx * bytes_per_px(k)));
+        RT_HIP(c->send[f.slot][k].ensure(send_bytes(pl, cam->width, nframes, k)));
         if (c->rank == 0) RT_HIP(c->recv[f.slot][k].ensure(npx * bytes_per_px(k) * c->nranks));
     }
     c->rows = pl.rows;
@@ -185,11 +205,13 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
         } else {
             for (auto& x : e.e) RT_HIP(hipEventCreate(&x));
         }
+        e.frames = nframes;
         f.ev = &e;
     }
     // the frame's own events replace the per-launch ones of the render
     pl.opts.flags &= ~(RT_FLAG_TIME_KERNEL | RT_FLAG_PIPELINE);
-    if (!(outputs & RT_OUT_LDR)) pl.opts.tonemap = RT_TONEMAP_NONE;
+    const bool ldr = (outputs & RT_OUT_LDR) || (local && local[2]);
+    if (!ldr) pl.opts.tonemap = RT_TONEMAP_NONE;
     else if (pl.opts.tonemap == RT_TONEMAP_NONE)
         return fail(RT_ERR_INVALID_ARG, "RT_OUT_LDR needs opts->tonemap");
     // the slot's buffers (and, for a serial frame, the caller's framebuffers) may still be in
@@ -202,8 +224,9 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
     if (pl.rows > 0) {
         void* out[3];
         for (int k = 0; k < 3; ++k)
-            out[k] = !(outputs & kOutputs[k]) ? nullptr : (f.direct ? dst[k] : c->send[f.slot][k].ptr);
-        st = enqueue_render(ctx, sc, cam, &pl.opts, static_cast<double*>(out[0]),
+            out[k] = !(outputs & kOutputs[k]) ? (local ? local[k] : nullptr)
+                                              : (f.direct ? dst[k] : c->send[f.slot][k].ptr);
+        st = enqueue_frames(ctx, sc, cams, nframes, &pl.opts, static_cast<double*>(out[0]),
                             static_cast<float*>(out[1]), static_cast<uint8_t*>(out[2]));
         if (st != RT_OK) return st;
     }
@@ -216,15 +239,23 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
     return record(f.ev, 2, f.gs);
 }
 
-// Phase 2: one ncclGather per output (inside the caller's group).
+// Phase 2: one ncclGather per frame and output (inside the caller's group, so that a batch's
+// gathers go out as one RCCL launch).  Frame j's rows start j·rows rows into the send buffer
+// and land j·n·max_rows rows into rank 0's receive buffer.
 rt_status gather_part(rt_comm* c, const rt_camera* cam, int outputs, const Frame& f) {
     if (f.direct) return RT_OK;
     const size_t npx = static_cast<size_t>(f.pl.max_rows) * cam->width;
+    const size_t own_px = static_cast<size_t>(f.pl.rows) * cam->width;
     for (int k = 0; k < 3; ++k) {
         if (!(outputs & kOutputs[k])) continue;
-        void* send = c->send[f.slot][k].ptr;
-        void* recv = c->rank == 0 ? c->recv[f.slot][k].ptr : send;
-        RT_NCCL(ncclGather(send, recv, npx * bytes_per_px(k), ncclUint8, 0, c->nccl, f.gs));
+        const size_t bpp = bytes_per_px(k);
+        for (int j = 0; j < f.nframes; ++j) {
+            char* send = static_cast<char*>(c->send[f.slot][k].ptr) + j * own_px * bpp;
+            char* recv = c->rank == 0 ? static_cast<char*>(c->recv[f.slot][k].ptr) +
+                                            j * npx * bpp * c->nranks
+                                      : send;
+            RT_NCCL(ncclGather(send, recv, npx * bpp, ncclUint8, 0, c->nccl, f.gs));
+        }
     }
     return RT_OK;
 }
@@ -251,16 +282,19 @@ rt_status gather_local(rt_comm* const* comms, int n, const rt_camera* cam, int o
     DeviceGuard g0(root->device);
     for (int k = 0; k < 3; ++k) {
         if (!(outputs & kOutputs[k])) continue;
-        const size_t bytes = npx * bytes_per_px(k);
-        char* recv = static_cast<char*>(root->recv[f0.slot][k].ptr);
-        for (int i = 0; i < n; ++i) {
-            const void* send = comms[i]->send[f[i].slot][k].ptr;
-            if (comms[i]->device == root->device)
-                RT_HIP(hipMemcpyAsync(recv + i * bytes, send, bytes, hipMemcpyDeviceToDevice,
-                                      f0.gs));
-            else
-                RT_HIP(hipMemcpyPeerAsync(recv + i * bytes, root->device, send,
-                                          comms[i]->device, bytes, f0.gs));
+        const size_t bpp = bytes_per_px(k), bytes = npx * bpp;
+        for (int j = 0; j < f0.nframes; ++j) {  // frame j: as gather_part lays it out
+            char* recv = static_cast<char*>(root->recv[f0.slot][k].ptr) + j * bytes * n;
+            for (int i = 0; i < n; ++i) {
+                const char* send = static_cast<const char*>(comms[i]->send[f[i].slot][k].ptr) +
+                                   j * static_cast<size_t>(f[i].pl.rows) * cam->width * bpp;
+                if (comms[i]->device == root->device)
+                    RT_HIP(hipMemcpyAsync(recv + i * bytes, send, bytes,
+                                          hipMemcpyDeviceToDevice, f0.gs));
+                else
+                    RT_HIP(hipMemcpyPeerAsync(recv + i * bytes, root->device, send,
+                                              comms[i]->device, bytes, f0.gs));
+            }
         }
     }
     RT_HIP(hipEventRecord(root->xfer_done, f0.gs));
@@ -283,7 +317,7 @@ rt_status assemble_part(rt_comm* c, const rt_camera* cam, int outputs, const Fra
             RT_HIP(launch_assemble_rows(c->recv[f.slot][k].ptr, dst[k],
                                         size_t(cam->width) * bytes_per_px(k), cam->height,
                                         f.pl.block, static_cast<uint32_t>(c->nranks),
-                                        f.pl.max_rows, f.gs));
+                                        f.pl.max_rows, static_cast<uint32_t>(f.nframes), f.gs));
         }
     }
     st = record(f.ev, 4, f.gs);
@@ -291,7 +325,10 @@ rt_status assemble_part(rt_comm* c, const rt_camera* cam, int outputs, const Fra
     if (f.pipelined) {
         RT_HIP(hipEventRecord(c->freed[f.slot], f.gs));
         c->slot_used[f.slot] = true;
+    } else {
+        RT_HIP(hipEventRecord(c->done, f.gs));
     }
+    c->any_frame = true;
     c->frame += 1;
     return RT_OK;
 }
@@ -301,6 +338,7 @@ rt_status init_streams(rt_comm* c) {
     RT_HIP(hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
     RT_HIP(hipEventCreateWithFlags(&c->xfer_ready, hipEventDisableTiming));
     RT_HIP(hipEventCreateWithFlags(&c->xfer_done, hipEventDisableTiming));
+    RT_HIP(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
     for (int s = 0; s < 2; ++s) {
         RT_HIP(hipEventCreateWithFlags(&c->rendered[s], hipEventDisableTiming));
         RT_HIP(hipEventCreateWithFlags(&c->freed[s], hipEventDisableTiming));
@@ -674,10 +712,15 @@ rt_status rt_comm_create_local(rt_context* const* ctxs, int n, rt_comm** out) {
 rt_status rt_comm_destroy(rt_comm* c) {
     if (!c) return RT_OK;
     DeviceGuard g(c->device);
-    // Renders into this comm's send buffers run on its context's stream, which may be any
-    // stream (rt_context_set_stream) of a context that may already be gone: wait for the whole
-    // device instead of dereferencing c->ctx.
-    (void)hipDeviceSynchronize();
+    // Every frame's last step is recorded on an event of this comm (`freed` of its slot when
+    // pipelined — its stream waited for the render first — else `done` on the render stream,
+    // which the gather and assembly share): wait for those, not for the whole device (other
+    // contexts' frames keep running).
+    if (c->any_frame) {
+        for (int s = 0; s < 2; ++s)
+            if (c->slot_used[s]) (void)hipEventSynchronize(c->freed[s]);
+        (void)hipEventSynchronize(c->done);
+    }
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
     for (auto* v : {&c->pending, &c->spare})
         for (auto& ev : *v)
@@ -692,6 +735,7 @@ rt_status rt_comm_destroy(rt_comm* c) {
     }
     if (c->xfer_ready) (void)hipEventDestroy(c->xfer_ready);
     if (c->xfer_done) (void)hipEventDestroy(c->xfer_done);
+    if (c->done) (void)hipEventDestroy(c->done);
     if (c->gstream) (void)hipStreamDestroy(c->gstream);
     delete c;
     return RT_OK;
@@ -709,32 +753,53 @@ rt_status rt_render_gather(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
                            const rt_render_opts* opts, int outputs, void* d_hdr64,
                            void* d_hdr32, void* d_ldr) {
     if (!c || !sc) return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_render_gather");
-    rt_status st = validate_camera(cam);
+    return rt_render_gather_batch(c, sc, cam, 1, opts, outputs, d_hdr64, d_hdr32, d_ldr,
+                                  nullptr, nullptr, nullptr);
+}
+
+rt_status rt_render_gather_batch(rt_comm* c, const rt_scene* sc, const rt_camera* cams,
+                                 int nframes, const rt_render_opts* opts, int outputs,
+                                 void* d_hdr64, void* d_hdr32, void* d_ldr, void* rank_hdr64,
+                                 void* rank_hdr32, void* rank_ldr) {
+    if (!c || !sc) return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_render_gather_batch");
+    rt_status st = check_batch(cams, nframes);
     if (st == RT_OK) st = check_outputs(outputs);
     void* const dst[3] = {d_hdr64, d_hdr32, d_ldr};
+    void* const local[3] = {rank_hdr64, rank_hdr32, rank_ldr};
     if (st == RT_OK) st = check_root_outputs(c, outputs, dst);
     if (st != RT_OK) return st;
+    for (int k = 0; k < 3; ++k)
+        if ((outputs & kOutputs[k]) && local[k])
+            return fail(RT_ERR_INVALID_ARG, "an output is either gathered or rank-local");
     if (c->local && c->nranks > 1)
         return fail(RT_ERR_INVALID_ARG, "local communicators (rt_comm_create_local) gather "
                                         "through rt_render_gather_all");
     DeviceGuard g(c->device);
     Frame f;
-    st = render_part(c, sc, cam, opts, outputs, dst, f);
+    st = render_part(c, sc, cams, nframes, opts, outputs, dst, local, f);
     if (st != RT_OK) return st;
     if (!f.direct) {
         RT_NCCL(ncclGroupStart());
-        st = gather_part(c, cam, outputs, f);
+        st = gather_part(c, cams, outputs, f);
         RT_NCCL(ncclGroupEnd());
         if (st != RT_OK) return st;
     }
-    return assemble_part(c, cam, outputs, f, dst);
+    return assemble_part(c, cams, outputs, f, dst);
 }
 
 rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, int n,
                                const rt_camera* cam, const rt_render_opts* opts, int outputs,
                                void* d_hdr64, void* d_hdr32, void* d_ldr) {
+    return rt_render_gather_all_batch(comms, scenes, n, cam, 1, opts, outputs, d_hdr64, d_hdr32,
+                                      d_ldr);
+}
+
+rt_status rt_render_gather_all_batch(rt_comm* const* comms, rt_scene* const* scenes, int n,
+                                     const rt_camera* cams, int nframes,
+                                     const rt_render_opts* opts, int outputs, void* d_hdr64,
+                                     void* d_hdr32, void* d_ldr) {
     if (!comms || !scenes || n < 1) return fail(RT_ERR_INVALID_ARG, "rt_render_gather_all: n < 1 or NULL");
-    rt_status st = validate_camera(cam);
+    rt_status st = check_batch(cams, nframes);
     if (st == RT_OK) st = check_outputs(outputs);
     if (st != RT_OK) return st;
     for (int i = 0; i < n; ++i)
@@ -750,24 +815,24 @@ rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, i
     std::vector<Frame> f(static_cast<size_t>(n));
     for (int i = 0; i < n; ++i) {  // 1. every GPU renders its rows (asynchronous)
         DeviceGuard g(comms[i]->device);
-        st = render_part(comms[i], scenes[i], cam, opts, outputs, dst, f[i]);
+        st = render_part(comms[i], scenes[i], cams, nframes, opts, outputs, dst, nullptr, f[i]);
         if (st != RT_OK) return st;
     }
     if (comms[0]->local) {  // 2. the gather as device copies into rank 0's receive buffer
-        st = gather_local(comms, n, cam, outputs, f);
+        st = gather_local(comms, n, cams, outputs, f);
         if (st != RT_OK) return st;
-    } else if (!f[0].direct) {  // 2. one gather per output over all GPUs
+    } else if (!f[0].direct) {  // 2. one gather per frame and output over all GPUs
         RT_NCCL(ncclGroupStart());
         for (int i = 0; i < n && st == RT_OK; ++i) {
             DeviceGuard g(comms[i]->device);
-            st = gather_part(comms[i], cam, outputs, f[i]);
+            st = gather_part(comms[i], cams, outputs, f[i]);
         }
         RT_NCCL(ncclGroupEnd());
         if (st != RT_OK) return st;
     }
     for (int i = 0; i < n; ++i) {  // 3. rank 0 assembles; the others close their events
         DeviceGuard g(comms[i]->device);
-        st = assemble_part(comms[i], cam, outputs, f[i], dst);
+        st = assemble_part(comms[i], cams, outputs, f[i], dst);
         if (st != RT_OK) return st;
     }
     return RT_OK;
@@ -805,7 +870,8 @@ rt_status rt_debug_assemble_rows(rt_context* ctx, const void* gathered, size_t r
     // the image at an offset that keeps the 16-B path when row_bytes allows it
     char* d_out = d_in + ((in_bytes + 15) & ~size_t(15));
     RT_HIP(hipMemcpyAsync(d_in, gathered, in_bytes, hipMemcpyHostToDevice, ctx->stream));
-    RT_HIP(launch_assemble_rows(d_in, d_out, row_bytes, height, block, n, max_rows, ctx->stream));
+    RT_HIP(launch_assemble_rows(d_in, d_out, row_bytes, height, block, n, max_rows, 1,
+                                ctx->stream));
     RT_HIP(hipMemcpyAsync(image, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(hipStreamSynchronize(ctx->stream));
     return RT_OK;

@@ -890,15 +890,15 @@ __host__ __device__ inline size_t pk_image_bytes(int ns, int np, int nl) {
     return (b + 15) / 16 * 16;
 }
 
-__device__ __forceinline__ void pk_build_image(const TraceParams& P, double* img, int tid,
-                                               int nthreads) {
+__device__ __forceinline__ void pk_build_image(const TraceParams& P, const double* camp,
+                                               double* img, int tid, int nthreads) {
     const int ns = P.ns, np = P.np, nl = P.nl, nb = pk_chunk_bounds(ns), nsb = ns + nb;
     double* s_sph = img;                                          // 80·nsb bytes
     double* s_pl = s_sph + kPkSph * nsb;
     double* s_lt = s_pl + kPlStride * np;
     double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
     int32_t* s_orig = reinterpret_cast<int32_t*>(s_pln + 4 * np);  // nb > 0 only
-    const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    const d3 cam = mk(camp[0], camp[1], camp[2]);
     const int32_t* perm = nb ? P.sph_perm : nullptr;
     for (int i = tid; i < nb; i += nthreads) {  // chunk bounds as pseudo-spheres ns + c
         const double* q = P.sph_bnd + 4 * i;
@@ -983,15 +983,30 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
     double* s_lt = s_pl + kPlStride * np;
     double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
     const int32_t* s_orig = reinterpret_cast<const int32_t*>(s_pln + 4 * np);
-    const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    // The frame: one per launch, or frame blockIdx.z of a batch (rt_render_batch) with its own
+    // camera and image source (scalar loads from the kernel arguments).
+    const double* camp = P.cam_pos;
+    const double* pk_img = P.pk_image;
+    unsigned long long* pk_pub = P.pk_pub;
+    uint32_t pk_epoch = P.pk_epoch;
+    uint64_t frame_off = 0;
+    if (P.nframes) {
+        const PkFrame& F = P.fr[blockIdx.z];
+        camp = F.cam;
+        pk_img = F.img;
+        pk_pub = F.pub;
+        pk_epoch = F.epoch;
+        frame_off = static_cast<uint64_t>(blockIdx.z) * P.frame_px;
+    }
+    const d3 cam = mk(camp[0], camp[1], camp[2]);
     constexpr int kThreads = 64 * kWgWavesX * WGY;
-    if (P.pk_image) {  // the image of this scene and camera, formed once (packet_image_kernel)
-        const float4* src = reinterpret_cast<const float4*>(P.pk_image);
+    if (pk_img) {  // the image of this scene and camera, formed once (packet_image_kernel)
+        const float4* src = reinterpret_cast<const float4*>(pk_img);
         float4* dst = reinterpret_cast<float4*>(smem);
         const int nv = static_cast<int>(pk_image_bytes(ns, np, nl) / 16);
         for (int i = tid; i < nv; i += kThreads) dst[i] = src[i];
         __syncthreads();
-    } else if (P.pk_pub) {
+    } else if (pk_pub) {
         // A camera without a cached image: the launch's first workgroup forms the image and
         // publishes it as {epoch, word} granules (8-byte agent-scope atomic stores, written
         // through to memory: the tag travels with its word, so no flag and no fence).  The
@@ -1003,16 +1018,16 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
         // stale or half-published slot just means "form it".
         uint32_t* dst = reinterpret_cast<uint32_t*>(smem);
         const int nw = static_cast<int>(pk_image_bytes(ns, np, nl) / 4);  // a multiple of 4
-        const uint32_t ep = P.pk_epoch;
-        const uint32_t wg = lin;
+        const uint32_t ep = pk_epoch;
+        const uint32_t wg = lin;  // in its frame: a batch's frames dispatch one after another
         bool have = false;
         if (wg >= P.pk_pub_first) {
             int ok = 1;
             for (int i = tid; i < nw / 2; i += kThreads) {
                 const unsigned long long gx = __hip_atomic_load(
-                    P.pk_pub + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    pk_pub + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long gy = __hip_atomic_load(
-                    P.pk_pub + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    pk_pub + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 ok &= static_cast<uint32_t>(gx >> 32) == ep && static_cast<uint32_t>(gy >> 32) == ep;
                 dst[2 * i] = static_cast<uint32_t>(gx);
                 dst[2 * i + 1] = static_cast<uint32_t>(gy);
@@ -1020,17 +1035,17 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
             have = __syncthreads_and(ok) != 0;
         }
         if (!have) {
-            pk_build_image(P, smem, tid, kThreads);
+            pk_build_image(P, camp, smem, tid, kThreads);
             __syncthreads();
             if (wg == 0) {
                 const unsigned long long tag = static_cast<unsigned long long>(ep) << 32;
                 for (int i = tid; i < nw; i += kThreads)
-                    __hip_atomic_store(P.pk_pub + i, tag | dst[i], __ATOMIC_RELAXED,
+                    __hip_atomic_store(pk_pub + i, tag | dst[i], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     } else {
-        pk_build_image(P, smem, tid, kThreads);
+        pk_build_image(P, camp, smem, tid, kThreads);
         __syncthreads();
     }
 
@@ -1222,7 +1237,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
         // accumulated / samples (Scene.h:298-300); x / 1.0 == x, so AA=1 skips the division
         const d3 v = samples == 1 ? acc
                    : (samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0));
-        const size_t o = static_cast<size_t>(yl_e) * P.width + x_e;
+        const size_t o = frame_off + static_cast<size_t>(yl_e) * P.width + x_e;
         if (P.out64) {
             P.out64[3 * o + 0] = v.x;
             P.out64[3 * o + 1] = v.y;
@@ -1261,7 +1276,8 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
         }
     }
     if constexpr (MULTI) {
-        if (P.tile_cost && lane == 0) {  // this wave's duration (100 MHz wall clock), per tile
+        // this wave's duration (100 MHz wall clock), per tile (a batch records its first frame)
+        if (P.tile_cost && lane == 0 && blockIdx.z == 0) {
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
             P.tile_cost[(tby * gridDim.x + tbx) * (kWgWavesX * WGY) + wave] =
                 static_cast<uint32_t>(t_end - t_start);
@@ -1277,7 +1293,7 @@ template __global__ void packet_direct_kernel<RT_PACKET_PROBE>(TraceParams);
 size_t packet_lds_bytes(int ns, int np, int nl) { return pk_image_bytes(ns, np, nl); }
 
 __global__ __launch_bounds__(256) void packet_image_kernel(TraceParams P, double* img) {
-    pk_build_image(P, img, static_cast<int>(threadIdx.x), 256);
+    pk_build_image(P, P.cam_pos, img, static_cast<int>(threadIdx.x), 256);
 }
 
 hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t stream) {
@@ -1390,7 +1406,7 @@ template <int MAXC, int FEAT, int WGY>
 static void launch_packet_shape(const TraceParams& p, bool count, size_t lds, hipStream_t stream) {
     const dim3 block(64 * kWgWavesX * WGY);
     const dim3 grid((p.width + kPkW * kWgWavesX - 1) / (kPkW * kWgWavesX),
-                    (p.rows + kPkH * WGY - 1) / (kPkH * WGY));
+                    (p.rows + kPkH * WGY - 1) / (kPkH * WGY), p.nframes ? p.nframes : 1u);
     // the single-sample variant keeps no accumulator live across the trace (AA = 1, the
     // reference default for a preview and the bench's configuration); counting passes use the
     // general one

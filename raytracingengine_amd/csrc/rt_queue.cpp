@@ -5,9 +5,9 @@
 // dependency between them (a camera's cached packet image, shared by frames on different
 // streams, is waited for through its own event — rt_capi.cpp packet_image) — except frames
 // that use scratch the context holds once: the breadth-first TraceRay arena of refraction-tree
-// scenes (ctx->wf / wf_ctl) and the ray counters.  Such a frame waits for the previous such
-// frame, on whichever stream it ran, so two of them never share the arena at once, and the
-// arena is never re-allocated under a frame still reading it.
+// scenes (ctx->wf / wf_ctl) and the ray counters.  enqueue_frames orders such a render after
+// the previous one on any stream of the context (scratch_wait / scratch_done, rt_capi.cpp), so
+// two of them never share the arena at once, whichever API enqueued them.
 #include <new>
 #include <string>
 #include <vector>
@@ -23,8 +23,6 @@ struct rt_queue {
     std::vector<hipStream_t> streams;
     std::vector<hipEvent_t> done;   // per slot: recorded after the slot's latest frame
     uint64_t next = 0;              // ticket of the next submitted frame (slot = ticket % depth)
-    hipEvent_t scratch_done = nullptr;  // after the latest frame that used the context's scratch
-    bool scratch_used = false;
 };
 
 extern "C" {
@@ -37,13 +35,6 @@ rt_status rt_queue_create(rt_context* ctx, int depth, rt_queue** out) {
     rt_queue* q = new (std::nothrow) rt_queue();
     if (!q) return fail(RT_ERR_OOM, "host allocation failed");
     q->ctx = ctx;
-    {
-        const hipError_t err = hipEventCreateWithFlags(&q->scratch_done, hipEventDisableTiming);
-        if (err != hipSuccess) {
-            rt_queue_destroy(q);
-            return hip_fail(err, "rt_queue_create");
-        }
-    }
     for (int i = 0; i < depth; ++i) {
         hipStream_t s = nullptr;
         hipEvent_t e = nullptr;
@@ -65,7 +56,6 @@ rt_status rt_queue_destroy(rt_queue* q) {
     DeviceGuard g(q->ctx->device);
     for (hipStream_t s : q->streams) (void)hipStreamSynchronize(s);
     for (hipEvent_t e : q->done) (void)hipEventDestroy(e);
-    if (q->scratch_done) (void)hipEventDestroy(q->scratch_done);
     for (hipStream_t s : q->streams) (void)hipStreamDestroy(s);
     delete q;
     return RT_OK;
@@ -79,9 +69,6 @@ rt_status rt_queue_submit(rt_queue* q, const rt_scene* sc, const rt_camera* cam,
     if (sc->ctx != ctx) return fail(RT_ERR_INVALID_ARG, "scene does not belong to the queue's context");
     DeviceGuard g(ctx->device);
     const size_t slot = static_cast<size_t>(q->next % q->streams.size());
-    const bool scratch = render_uses_context_scratch(sc, opts);
-    // serialised behind the previous frame that used the context's scratch (any stream)
-    if (scratch && q->scratch_used) RT_HIP(hipStreamWaitEvent(q->streams[slot], q->scratch_done, 0));
     // the render goes through the context's launch path on the slot's stream
     hipStream_t saved = ctx->stream;
     ctx->stream = q->streams[slot];
@@ -89,10 +76,6 @@ rt_status rt_queue_submit(rt_queue* q, const rt_scene* sc, const rt_camera* cam,
                                   static_cast<float*>(d_hdr32), static_cast<uint8_t*>(d_ldr));
     hipError_t e = hipSuccess;
     if (st == RT_OK) e = hipEventRecord(q->done[slot], q->streams[slot]);
-    if (st == RT_OK && e == hipSuccess && scratch) {
-        e = hipEventRecord(q->scratch_done, q->streams[slot]);
-        q->scratch_used = true;
-    }
     ctx->stream = saved;
     if (st != RT_OK) return st;
     if (e != hipSuccess) return hip_fail(e, "rt_queue_submit");

@@ -1,0 +1,279 @@
+"""Frame batches (rt_render_batch, rt_render_gather_batch, rt_render_gather_all_batch): several
+frames of one scene — one camera position each — in one packet-kernel launch (one grid plane per
+frame), each frame the frame rt_render gives for its camera (RE/Scene.h:311-328), and the
+multi-rank batch layouts (padded send rows, per-frame gathers, per-frame assembly) end to end."""
+import dataclasses
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from raytracingengine_amd import capi
+from raytracingengine_amd.configs import make_config
+
+pytestmark = pytest.mark.gpu
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _positions(ds, n, seed=7):
+    """n camera positions around the scene's own: the base position (cached image after its
+    second sighting) mixed with moves seen once (hand-off slot / per-workgroup image)."""
+    base = ds.camera["position"][0].copy()
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        out.append(base if i % 3 == 0 else base + rng.uniform(-0.5, 0.5, 3))
+    return np.array(out)
+
+
+def _single(ds, pos, opts, rows, w):
+    """The frame of one camera position through rt_render_device (synchronous copy)."""
+    saved = ds.camera["position"][0].copy()
+    ds.camera["position"][0] = pos
+    try:
+        h = torch.empty(rows * w * 3, dtype=torch.float64, device="cuda")
+        l = torch.empty(rows * w * 3, dtype=torch.uint8, device="cuda")
+        ds.render_device(h.data_ptr(), None, l.data_ptr(), opts)
+        ds.ctx.synchronize()
+        return h.cpu().numpy(), l.cpu().numpy()
+    finally:
+        ds.camera["position"][0] = saved
+
+
+@pytest.mark.parametrize("name,w,h,n", [("c2", 480, 270, 1), ("c2", 480, 270, 5),
+                                        ("c2", 480, 270, 16), ("c2", 320, 180, 21),
+                                        ("c3", 480, 270, 6), ("c5", 320, 180, 4),
+                                        ("c4", 400, 240, 3), ("mesh", 320, 180, 3),
+                                        ("bigmesh", 320, 180, 3), ("mirror", 240, 160, 3),
+                                        ("glass", 160, 120, 2)])
+def test_batch_frames_equal_single_renders(ctx, name, w, h, n):
+    """Every frame of a batch equals rt_render_device of its camera, bit for bit (HDR and
+    Reinhard bytes): packet scenes in one launch per 16 frames (C2-C5, triangles), chain and
+    tree scenes one launch per frame.  Repeated, cached and first-seen cameras mixed."""
+    sc = make_config(name, w, h)
+    ds = ctx.scene(sc)
+    try:
+        pos = _positions(ds, n)
+        opts = capi.default_opts(tonemap=1)
+        refs = [_single(ds, p, opts, h, w) for p in pos]
+        for rnd in range(2):  # the second round sees every camera again (cached images)
+            H64 = torch.full((n * h * w * 3,), -1.0, dtype=torch.float64, device="cuda")
+            L8 = torch.zeros(n * h * w * 3, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            ds.render_batch(ds.cameras(pos), H64.data_ptr(), None, L8.data_ptr(), opts)
+            ctx.synchronize()
+            a64 = H64.cpu().numpy().reshape(n, -1)
+            a8 = L8.cpu().numpy().reshape(n, -1)
+            for f in range(n):
+                assert np.array_equal(a64[f], refs[f][0]), (rnd, f)
+                assert np.array_equal(a8[f], refs[f][1]), (rnd, f)
+    finally:
+        ds.close()
+
+
+def test_batch_moved_camera_vs_oracle(ctx, oracle):
+    """A batch frame from a moved camera against the C oracle rendering that camera."""
+    sc = make_config("c2", 192, 108)
+    ds = ctx.scene(sc)
+    try:
+        base = np.array(sc.camera.position)
+        pos = np.array([base, base + (0.3, -0.2, 0.5), base + (-0.7, 0.1, 1.0)])
+        H64 = torch.empty(3 * 108 * 192 * 3, dtype=torch.float64, device="cuda")
+        ds.render_batch(ds.cameras(pos), H64.data_ptr(), None, None, capi.default_opts(tonemap=-1))
+        ctx.synchronize()
+        got = H64.cpu().numpy().reshape(3, 108, 192, 3)
+    finally:
+        ds.close()
+    for f in range(3):
+        scf = dataclasses.replace(sc, camera=dataclasses.replace(sc.camera,
+                                                                 position=tuple(pos[f])))
+        ref, _, _ = oracle.render(scf)
+        assert np.array_equal(got[f], ref), f
+
+
+def test_batch_full_c2_static_camera_is_the_reference(ctx, golden):
+    """The bench's batch: four 1920x1080 C2 frames of the static camera in one launch — each
+    frame's HDR and Reinhard bytes have the reference's SHA-256."""
+    info = golden["meta"]["scenes"]["c2_full"]
+    sc = make_config("c2")
+    ds = ctx.scene(sc)
+    W, H = sc.camera.width, sc.camera.height
+    try:
+        cams = ds.cameras(np.repeat(ds.camera["position"], 4, axis=0))
+        H64 = torch.empty(4 * H * W * 3, dtype=torch.float64, device="cuda")
+        L8 = torch.empty(4 * H * W * 3, dtype=torch.uint8, device="cuda")
+        for _ in range(3):  # fresh camera, cache-creating and cached launches
+            H64.zero_()
+            L8.zero_()
+            torch.cuda.synchronize()
+            ds.render_batch(cams, H64.data_ptr(), None, L8.data_ptr(), capi.default_opts(tonemap=1))
+            ctx.synchronize()
+            a64 = H64.cpu().numpy().reshape(4, -1)
+            a8 = L8.cpu().numpy().reshape(4, -1)
+            for f in range(4):
+                assert _sha(a64[f]) == info["image_sha256"], f
+                assert _sha(a8[f]) == info["ldr_sha256"]["reinhard_simple"], f
+    finally:
+        ds.close()
+
+
+def test_batch_row_sets_equal_single_row_renders(ctx):
+    """A rank's block-cyclic rows of every frame of a batch = its single-frame row renders."""
+    sc = make_config("c3", 480, 270)
+    ds = ctx.scene(sc)
+    try:
+        pos = _positions(ds, 4, seed=3)
+        o = capi.default_opts(tonemap=1, row_begin=32, row_end=270, row_block=16, row_cycle=3)
+        rows = capi.rendered_rows(o, 270)
+        refs = [_single(ds, p, o, rows, 480) for p in pos]
+        H64 = torch.empty(4 * rows * 480 * 3, dtype=torch.float64, device="cuda")
+        L8 = torch.empty(4 * rows * 480 * 3, dtype=torch.uint8, device="cuda")
+        ds.render_batch(ds.cameras(pos), H64.data_ptr(), None, L8.data_ptr(), o)
+        ctx.synchronize()
+        a64 = H64.cpu().numpy().reshape(4, -1)
+        a8 = L8.cpu().numpy().reshape(4, -1)
+        for f in range(4):
+            assert np.array_equal(a64[f], refs[f][0]), f
+            assert np.array_equal(a8[f], refs[f][1]), f
+    finally:
+        ds.close()
+
+
+def test_batch_ray_counts_are_the_sum_of_frames(ctx):
+    """RT_FLAG_COUNT_RAYS over a batch counts every frame's rays (the counting launch is a
+    batch too)."""
+    sc = make_config("c2", 320, 180)
+    ds = ctx.scene(sc)
+    try:
+        pos = _positions(ds, 3, seed=11)
+        total = 0
+        for p in pos:
+            ds.camera["position"][0] = p
+            out = ds.render(hdr64=True, stats=True)
+            total += out["trace_rays"] + out["shadow_rays"]
+        ds.camera["position"][0] = pos[0]
+        H64 = torch.empty(3 * 180 * 320 * 3, dtype=torch.float64, device="cuda")
+        ctx.reset_stats()
+        ds.render_batch(ds.cameras(pos), H64.data_ptr(), None, None,
+                        capi.default_opts(tonemap=-1, flags=capi.RT_FLAG_COUNT_RAYS))
+        st = ctx.stats()
+        assert st.trace_rays + st.shadow_rays == total
+    finally:
+        ds.close()
+
+
+def test_batch_rejects_mismatched_cameras(ctx):
+    sc = make_config("c2", 64, 32)
+    ds = ctx.scene(sc)
+    try:
+        cams = ds.cameras(np.repeat(ds.camera["position"], 2, axis=0))
+        cams["width"][1] = 65
+        buf = torch.empty(2 * 65 * 32 * 3, dtype=torch.float64, device="cuda")
+        with pytest.raises(capi.RtError) as e:
+            ds.render_batch(cams, buf.data_ptr(), None, None, capi.default_opts(tonemap=-1))
+        assert e.value.status == capi.RT_ERR_INVALID_ARG
+        with pytest.raises(capi.RtError) as e:
+            ds.render_batch(cams[:0], buf.data_ptr(), None, None, capi.default_opts(tonemap=-1))
+        assert e.value.status == capi.RT_ERR_INVALID_ARG
+    finally:
+        ds.close()
+
+
+# ------------------------------------------------------------------ gathered batches
+@pytest.fixture(scope="module")
+def comm1(ctx):
+    c = capi.Comm(ctx, 1, 0, capi.comm_unique_id())
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_gather_batch_one_rank_ldr_gathered_hdr_local(ctx, comm1, pipeline):
+    """The bench's step at N = 1: rt_render_gather_batch with the Reinhard bytes gathered
+    (here: rendered straight into the frame) and the f64 HDR kept rank-local; three batches in
+    a row through the pipelined slots.  Every frame = its single render."""
+    sc = make_config("c2", 480, 270)
+    W, H, n = 480, 270, 4
+    ds = ctx.scene(sc)
+    try:
+        pos = _positions(ds, n, seed=5)
+        opts = capi.default_opts(tonemap=1, flags=capi.RT_FLAG_PIPELINE if pipeline else 0)
+        refs = [_single(ds, p, capi.default_opts(tonemap=1), H, W) for p in pos]
+        outs = []
+        for b in range(3):
+            L8 = torch.zeros(n * H * W * 3, dtype=torch.uint8, device="cuda")
+            R64 = torch.zeros(n * H * W * 3, dtype=torch.float64, device="cuda")
+            torch.cuda.synchronize()
+            comm1.render_gather_batch(ds, ds.cameras(pos), opts, capi.RT_OUT_LDR,
+                                      d_ldr=L8.data_ptr(), rank_hdr64=R64.data_ptr())
+            outs.append((L8, R64))
+        comm1.synchronize()
+        ctx.synchronize()
+        for b, (L8, R64) in enumerate(outs):
+            a8 = L8.cpu().numpy().reshape(n, -1)
+            a64 = R64.cpu().numpy().reshape(n, -1)
+            for f in range(n):
+                assert np.array_equal(a8[f], refs[f][1]), (b, f)
+                assert np.array_equal(a64[f], refs[f][0]), (b, f)
+    finally:
+        ds.close()
+
+
+def test_gather_batch_rejects_gathered_and_local_output(ctx, comm1):
+    sc = make_config("c2", 64, 32)
+    ds = ctx.scene(sc)
+    try:
+        buf = torch.empty(64 * 32 * 3, dtype=torch.float64, device="cuda")
+        with pytest.raises(capi.RtError) as e:
+            comm1.render_gather_batch(ds, ds.cameras(ds.camera["position"]),
+                                      capi.default_opts(tonemap=-1), capi.RT_OUT_HDR64,
+                                      d_hdr64=buf.data_ptr(), rank_hdr64=buf.data_ptr())
+        assert e.value.status == capi.RT_ERR_INVALID_ARG
+    finally:
+        ds.close()
+
+
+@pytest.mark.parametrize("name,w,h,ranks,block,nf", [("c2", 480, 270, 8, 16, 4),
+                                                     ("c2", 480, 270, 3, 16, 5),
+                                                     ("c3", 320, 180, 4, 8, 3),
+                                                     ("c2", 200, 40, 4, 16, 2)])
+def test_gather_all_batch_local_ranks_is_the_frames(name, w, h, ranks, block, nf):
+    """The multi-rank batch on one GPU through local communicators: every rank renders its
+    block-cyclic rows of every frame in one launch into a padded send buffer (frame f at f·rows,
+    max_rows sent from there), rank 0 receives frame f's chunks at f·n·max_rows and assembles
+    all frames in one launch.  Ranks with fewer rows (200x40 over 4 ranks of 16-row blocks:
+    one rank has none) included.  Every frame = the single-rank frame."""
+    ctxs = [capi.Context(0) for _ in range(ranks)]
+    try:
+        comms = capi.Comm.create_local(ctxs)
+        sc = make_config(name, w, h)
+        scenes = [c.scene(sc) for c in ctxs]
+        pos = _positions(scenes[0], nf, seed=13)
+        refs = [_single(scenes[0], p, capi.default_opts(tonemap=1), h, w) for p in pos]
+        for pipeline in (False, True):
+            opts = capi.default_opts(tonemap=1, row_block=block,
+                                     flags=capi.RT_FLAG_PIPELINE if pipeline else 0)
+            L8 = torch.zeros(nf * h * w * 3, dtype=torch.uint8, device="cuda")
+            H64 = torch.zeros(nf * h * w * 3, dtype=torch.float64, device="cuda")
+            torch.cuda.synchronize()
+            capi.render_gather_all_batch(comms, scenes, scenes[0].cameras(pos), opts,
+                                         capi.RT_OUT_LDR | capi.RT_OUT_HDR64,
+                                         d_hdr64=H64.data_ptr(), d_ldr=L8.data_ptr())
+            for c in comms:
+                c.synchronize()
+            a8 = L8.cpu().numpy().reshape(nf, -1)
+            a64 = H64.cpu().numpy().reshape(nf, -1)
+            for f in range(nf):
+                assert np.array_equal(a8[f], refs[f][1]), (pipeline, f)
+                assert np.array_equal(a64[f], refs[f][0]), (pipeline, f)
+        for s in scenes:
+            s.close()
+        for c in comms:
+            c.close()
+    finally:
+        for c in ctxs:
+            c.close()

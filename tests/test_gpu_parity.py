@@ -196,29 +196,6 @@ def test_full_c2_sha256_matches_reference(ctx, golden):
     assert out["trace_rays"] == 1920 * 1080
 
 
-def test_full_c1_reference_box(ctx, golden):
-    sc = make_config("c1")
-    out = _render(ctx, sc, hdr64=True)
-    sub = golden["full"]["c1"]
-    got = out["hdr64"].reshape(-1, 3)[::golden["meta"]["scenes"]["c1_full"]["subsample_stride"]]
-    assert np.abs(got - sub).max() <= POW_TOL
-
-
-@pytest.mark.parametrize("name", ["c3", "c4", "c5"])
-def test_full_size_spot_rows_vs_oracle(ctx, oracle, name):
-    """At full BASELINE resolution: oracle rows spread over the frame must match exactly."""
-    sc = make_config(name)
-    H = sc.camera.height
-    ds = ctx.scene(sc)
-    try:
-        for r in (0, H // 3, H // 2 + 1, H - 1):
-            out = ds.render(hdr64=True, row_begin=r, row_end=r + 1)
-            ref, _, _ = oracle.render(sc, rows=(r, r + 1))
-            assert np.array_equal(out["hdr64"], ref), (name, r)
-    finally:
-        ds.close()
-
-
 @pytest.mark.parametrize("name", ["c2", "mirror"])
 def test_row_tiles_equal_full_frame(ctx, name):
     """Row tiles (the multi-GPU split) reassemble to the full frame byte for byte."""

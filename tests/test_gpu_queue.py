@@ -78,6 +78,52 @@ def test_queue_full_c2_matches_reference(ctx, golden):
         ds.close()
 
 
+def test_queue_alternating_launch_shapes_keep_their_tile_orders(ctx):
+    """One camera, launches of different shapes in flight together on three streams: whole
+    frames at two resolutions, a block-cyclic row set and a contiguous row range.  Each shape
+    records, builds and then dispatches by its own costliest-first tile order (rt_capi.cpp
+    tile_order: one entry per shape, never rewritten while a launch of another shape may read
+    it).  Every frame equals the synchronous render of its shape."""
+    sc = make_config("c3", 640, 360)
+    ds = ctx.scene(sc)
+    q = capi.Queue(ctx, 3)
+    W, H = sc.camera.width, sc.camera.height
+    shapes = [((W, H), capi.default_opts(tonemap=1)),
+              ((W // 2, H // 2), capi.default_opts(tonemap=1)),
+              ((W, H), capi.default_opts(tonemap=1, row_begin=16, row_end=H, row_block=16,
+                                         row_cycle=3)),
+              ((W, H), capi.default_opts(tonemap=1, row_begin=40, row_end=200))]
+    try:
+        refs = []
+        for (w, h), o in shapes:
+            ds.camera["width"], ds.camera["height"] = w, h
+            rows = capi.rendered_rows(o, h)
+            hd = torch.empty(rows * w * 3, dtype=torch.float64, device="cuda")
+            ld = torch.empty(rows * w * 3, dtype=torch.uint8, device="cuda")
+            ds.render_device(hd.data_ptr(), None, ld.data_ptr(), o)
+            ctx.synchronize()
+            refs.append((hd.cpu().numpy(), ld.cpu().numpy()))
+        n = 24   # every shape: cache creation, recording, order build, ordered launches
+        bufs = []
+        for i in range(n):
+            k = i % len(shapes)
+            (w, h), o = shapes[k]
+            ds.camera["width"], ds.camera["height"] = w, h
+            rows = capi.rendered_rows(o, h)
+            hd = torch.empty(rows * w * 3, dtype=torch.float64, device="cuda")
+            ld = torch.empty(rows * w * 3, dtype=torch.uint8, device="cuda")
+            q.submit(ds, o, hd.data_ptr(), None, ld.data_ptr())
+            bufs.append((k, hd, ld))
+        q.synchronize()
+        for i, (k, hd, ld) in enumerate(bufs):
+            assert np.array_equal(hd.cpu().numpy(), refs[k][0]), (i, k)
+            assert np.array_equal(ld.cpu().numpy(), refs[k][1]), (i, k)
+    finally:
+        ds.camera["width"], ds.camera["height"] = W, H
+        q.close()
+        ds.close()
+
+
 def test_queue_rejects_bad_arguments(ctx):
     with pytest.raises(capi.RtError) as e:
         capi.Queue(ctx, 0)
