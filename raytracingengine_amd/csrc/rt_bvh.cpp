@@ -5,7 +5,9 @@
 //
 // Binned SAH over triangle centroids, leaves of <= 4 triangles, depth <= 48.  Node layout (8
 // doubles, 64 B): lo xyz, hi xyz, then {int32 first, int32 count} in the bits of slot 6; count
-// == 0 marks an internal node whose children are nodes first and first + 1.  Boxes are widened
+// == 0 marks an internal node whose children are nodes first and first + 1 (the child of the
+// lower centroids first), and slot 7 holds its split axis (int32 0..2; the wave-coherent
+// traversal of the packet kernel visits the child nearer along it first).  Boxes are widened
 // by 1e-9 of their extent and coordinates plus 1e-300 so that every hit the FP64
 // Möller-Trumbore test accepts lies strictly inside its leaf's box.
 #include <algorithm>
@@ -55,7 +57,7 @@ struct Builder {
         nodes.resize(nodes.size() + kBvhNodeStride, 0.0);
         return static_cast<int32_t>(nodes.size() / kBvhNodeStride - 1);
     }
-    void write(int32_t n, const Box& b, int32_t first, int32_t count) {
+    void write(int32_t n, const Box& b, int32_t first, int32_t count, int32_t axis = 0) {
         double* o = &nodes[size_t(n) * kBvhNodeStride];
         for (int k = 0; k < 3; ++k) {
             const double m = 1e-9 * ((b.hi[k] - b.lo[k]) + std::max(std::fabs(b.lo[k]),
@@ -66,7 +68,8 @@ struct Builder {
         }
         int32_t fc[2] = {first, count};
         std::memcpy(&o[6], fc, sizeof fc);
-        o[7] = 0.0;
+        const int32_t ax[2] = {axis, 0};
+        std::memcpy(&o[7], ax, sizeof ax);
     }
     // builds prims[b, e) into node n
     void build(int32_t n, size_t b, size_t e, int depth) {
@@ -122,12 +125,14 @@ struct Builder {
             }
         }
         size_t mid;
+        int32_t split_axis = best_axis;
         if (best_axis < 0) {
             // no useful SAH split: median on the longest centroid axis (or a leaf of equal
             // centroids when it cannot be split)
             int k = 0;
             for (int a = 1; a < 3; ++a)
                 if (cbox.hi[a] - cbox.lo[a] > cbox.hi[k] - cbox.lo[k]) k = a;
+            split_axis = k;
             if (!(cbox.hi[k] > cbox.lo[k])) {
                 if (count <= 16) {
                     write(n, box, static_cast<int32_t>(b), static_cast<int32_t>(count));
@@ -152,7 +157,7 @@ struct Builder {
         }
         const int32_t left = alloc();
         alloc();  // right = left + 1
-        write(n, box, left, 0);
+        write(n, box, left, 0, split_axis);
         build(left, b, mid, depth + 1);
         build(left + 1, mid, e, depth + 1);
     }

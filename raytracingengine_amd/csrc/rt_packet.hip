@@ -73,6 +73,14 @@ constexpr int kFeatNoPL = 32;
 // Waves per SIMD of the single-sample variant for <= 64 spheres, point lights and no other
 // feature (C2): 6 with its light records read through the scalar cache (80 VGPRs, 48 B/lane of
 // scratch): C2 48.1 -> 46.7 us against 5 waves (95 VGPRs + 20 B, lights from LDS), MI355X
+// The single-sample lean variant (C2) parks the hit point, normal and diffuse sum of its lanes
+// in LDS while a wave runs the (rare) exact shadow march, so that the march's registers do not
+// force spills on the common path (RT_PK_MARCH_SAVE: 0 off, 1 on).
+#ifndef RT_PK_MARCH_SAVE
+#define RT_PK_MARCH_SAVE 0
+#endif
+constexpr int kPkSaveDoubles = 9;  // per lane: hp, n, diff
+constexpr int kPkStack = 64;       // wave-coherent BVH walk: node stack entries per wave (depth ≤ 48)
 #ifndef RT_PACKET_SMALL_WAVES
 #define RT_PACKET_SMALL_WAVES 6
 #endif
@@ -92,6 +100,22 @@ constexpr int kFeatNoPL = 32;
 #ifndef RT_PACKET_AA1_WAVES
 #define RT_PACKET_AA1_WAVES 5
 #endif
+
+// This lane's index in the wave, formed where it is used: an opaque (volatile) mbcnt pair the
+// compiler cannot hoist and keep live — it spilled the hoisted lane·80 LDS offset of the culls
+// in the C2 variant (RT_PK_OPAQUE_LANE: 0 threadIdx.x & 63, 1 opaque).
+#ifndef RT_PK_OPAQUE_LANE
+#define RT_PK_OPAQUE_LANE 0
+#endif
+__device__ __forceinline__ int cull_lane() {
+#if RT_PK_OPAQUE_LANE
+    int l;
+    __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+#else
+    return static_cast<int>(threadIdx.x & 63);
+#endif
+}
 
 // ------------------------------------------------------------------ wave reductions (FP32)
 // Every lane must be active.  Floats are reduced as order-preserving int32 keys (sign-magnitude
@@ -152,6 +176,7 @@ struct PacketScene {
     // and orig[i] is sorted sphere i's index in the scene (material table, closest-hit ties)
     const int32_t* orig;
     int ns, np, nt, nl, nb;
+    int* wstk;  // LDS: this wave's node stack of the wave-coherent BVH walk (kFeatTris variants)
 };
 
 // Closest hit of the packet kernel: t and the primitive's index in the material table order
@@ -228,7 +253,7 @@ __device__ __forceinline__ void cone_terms(const double* s, double radius, d3 o,
 template <int MAXC>
 __device__ __forceinline__ Masks<MAXC> cull_cone(const PacketScene& S, d3 axis, double cos_min) {
     Masks<MAXC> M;
-    const int lane = threadIdx.x & 63;
+    const int lane = cull_lane();
     const float cs = static_cast<float>(cos_min) * (1.0f - 1e-6f);  // rounded down (cs > 0)
     const float sn = sqrt_f32(fmaxf(0.0f, 1.0f - cs * cs)) * (1.0f + 1e-5f);  // rounded up
     const float ax = static_cast<float>(axis.x), ay = static_cast<float>(axis.y),
@@ -270,7 +295,7 @@ template <int MAXC, int FEAT>
 __device__ __forceinline__ Masks<MAXC> cull_capsule(const PacketScene& S, d3 c, float R, d3 L,
                                                     double RL, double bias) {
     Masks<MAXC> M;
-    const int lane = threadIdx.x & 63;
+    const int lane = cull_lane();
     const float sx = static_cast<float>(L.x - c.x), sy = static_cast<float>(L.y - c.y),
                 sz = static_cast<float>(L.z - c.z);
     const float sl2 = dot3f(sx, sy, sz, sx, sy, sz);
@@ -456,6 +481,76 @@ __device__ __forceinline__ void plane_t_core(double num, double denom, int p, bo
     }
 }
 
+// The triangles' part of IntersectClosest over the BVH, walked once per WAVE (the packet
+// kernel's rays of an 8x8 tile, or the lanes of a shadow march, go through the same nodes):
+// the node stack is wave-uniform in LDS, node boxes, leaf triangle ids and triangle records
+// are read through the scalar cache (wave-uniform addresses: SGPRs, no per-lane loads), and
+// each lane tests the popped node's box against its own current best (the per-lane walk's
+// test, bvh_triangles in rt_trace_common.hpp, with the same 1e-9 margin), so a lane only tests
+// the triangles of leaves its ray reaches and is not closer than.  A lane may see nodes its
+// own walk would not visit (another lane hit them); every triangle it tests in a leaf is a real
+// intersection test, so it still returns exactly the (t, index) minimum among the triangles
+// the reference tests (the leaf of the winning triangle is always entered: every ancestor box
+// contains the hit, and no box whose entry exceeds the winner's t is needed).  Children are
+// pushed nearer-first along the node's split axis by the lanes' majority direction.
+typedef const __attribute__((address_space(4))) int32_t* pk_cip;
+typedef const __attribute__((address_space(4))) double* pk_cdp;
+__device__ __forceinline__ void bvh_wave(const PacketScene& S, d3 o, d3 d, bool& found,
+                                         double& best, int& kind, int& idx) {
+    const d3 inv = mk(d.x != 0.0 ? 1.0 / d.x : 0.0, d.y != 0.0 ? 1.0 / d.y : 0.0,
+                      d.z != 0.0 ? 1.0 / d.z : 0.0);
+    const pk_cdp bvh = (pk_cdp)S.bvh;
+    const pk_cdp tri = (pk_cdp)S.tri;
+    const pk_cip ord = (pk_cip)S.bvh_tri;
+    int* stk = S.wstk;
+    bool tf = false;
+    double tb = 0.0;
+    int ti = 0;
+    int sp = 0;
+    stk[sp++] = 0;  // every active lane writes the same value
+    while (sp > 0) {
+        const int node = __builtin_amdgcn_readfirstlane(stk[--sp]);
+        const pk_cdp nd = bvh + kBvhNodeStride * node;
+        const double bound = tf ? (found ? fmin(tb, best) : tb) : (found ? best : INFINITY);
+        double tn;
+        const bool in = bvh_box_v(mk(nd[0], nd[1], nd[2]), mk(nd[3], nd[4], nd[5]), o, d, inv, tn) &&
+                        !(tn > bound * (1.0 + 1e-9));
+        if (__ballot(in) == 0) continue;  // uniform
+        const double w = nd[6];
+        const int first = __double2loint(w), count = __double2hiint(w);
+        if (count > 0) {
+            if (in) {
+                for (int j = first; j < first + count; ++j) {
+                    const int i = ord[j];
+                    const pk_cdp q = tri + kTriStride * i;
+                    double t;
+                    if (tri_hit_v(mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8]),
+                                  o, d, t) &&
+                        (!tf || t < tb || (t == tb && i < ti))) {
+                        tf = true;
+                        tb = t;
+                        ti = i;
+                    }
+                }
+            }
+            continue;
+        }
+        const int axis = __double2loint(nd[7]);
+        const double da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+        const int pos = __builtin_popcountll(__ballot(in && da > 0.0));
+        const int neg = __builtin_popcountll(__ballot(in && da < 0.0));
+        const bool low_first = pos >= neg;  // the lower child is nearer for rays going up
+        stk[sp++] = low_first ? first + 1 : first;
+        stk[sp++] = low_first ? first : first + 1;
+    }
+    if (tf && (!found || tb < best)) {
+        found = true;
+        best = tb;
+        kind = 3;
+        idx = ti;
+    }
+}
+
 template <int FEAT>
 __device__ __forceinline__ void triangles(const PacketScene& S, d3 o, d3 d, bool& found,
                                           double& best, int& prim) {
@@ -463,7 +558,7 @@ __device__ __forceinline__ void triangles(const PacketScene& S, d3 o, d3 d, bool
     const int base = S.ns + S.np;
     if (S.bvh) {
         int kind = 0, ti = -1;
-        bvh_triangles(S.tri, S.bvh, S.bvh_tri, o, d, found, best, kind, ti);
+        bvh_wave(S, o, d, found, best, kind, ti);
         if (kind == 3) prim = base + ti;
         return;
     }
@@ -736,10 +831,11 @@ __device__ __forceinline__ Masks<MAXC> shadow_masks(const PacketScene& S, bool c
 // One light of directLightning (Scene.h:86-124) for the whole wave: every lane calls it
 // (uniform control flow for the packet reductions); `active` lanes shade.
 template <int MAXC, int FEAT, bool COUNT>
-__device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P, d3 n, d3 view,
+__device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3& P, d3& n, d3 view,
                                          const PkHit& h, d3 lpos, d3 E, d3 lcenter, double lrad,
                                          double bias, int nchunks, d3& diff, d3& spec,
-                                         Counts& cnt, const Masks<MAXC>* pre = nullptr) {
+                                         Counts& cnt, const Masks<MAXC>* pre = nullptr,
+                                         double* save = nullptr, int tid = 0, int nthr = 0) {
     double dist = 0.0, inv_d2 = 0.0;
     d3 L = mk(0.0, 0.0, 0.0);
     if (active) light_dir(lpos - P, dist, L, inv_d2);  // skipped by waves with no hit lane
@@ -835,7 +931,30 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
             for (int c = 0; c < MAXC; ++c) Mu.m[c] &= t.m[c];
             Mu.pm &= t.pm;
         }
+        // `save`: this lane's hit point, normal and diffuse sum go to LDS (structure of arrays,
+        // conflict-free) for the march and come back after it; the empty asm keeps the compiler
+        // from forwarding the stored values, so their registers are free inside the march
+        if (save) {
+            double* q = save + tid;
+            q[0 * nthr] = P.x;
+            q[1 * nthr] = P.y;
+            q[2 * nthr] = P.z;
+            q[3 * nthr] = n.x;
+            q[4 * nthr] = n.y;
+            q[5 * nthr] = n.z;
+            q[6 * nthr] = diff.x;
+            q[7 * nthr] = diff.y;
+            q[8 * nthr] = diff.z;
+            __asm__ volatile("" ::: "memory");
+        }
         if (undecided) T = pk_transmittance<MAXC, FEAT>(S, Mu, nchunks, so, L, dist - bias, bias);
+        if (save) {
+            __asm__ volatile("" ::: "memory");
+            const double* q = save + tid;
+            P = mk(q[0 * nthr], q[1 * nthr], q[2 * nthr]);
+            n = mk(q[3 * nthr], q[4 * nthr], q[5 * nthr]);
+            diff = mk(q[6 * nthr], q[7 * nthr], q[8 * nthr]);
+        }
     }
     if (!need) return;
     if (COUNT) cnt.shadow++;
@@ -858,7 +977,6 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
 // is read through the scalar cache: wave-uniform, so SGPRs instead of VGPRs, which is what lets
 // C2's variant run at 6 waves/SIMD (RT_PACKET_SMALL_WAVES).  More spheres keep the LDS copy
 // (C3 +1.2 % through the scalar cache: the chunk masks need those SGPRs).
-typedef const __attribute__((address_space(4))) double* pk_cdp;
 template <int MAXC>
 __device__ __forceinline__ void pk_light_record(const PacketScene& S, const TraceParams& P, int l,
                                                 d3& L, d3& E) {
@@ -983,6 +1101,8 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
     double* s_lt = s_pl + kPlStride * np;
     double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
     const int32_t* s_orig = reinterpret_cast<const int32_t*>(s_pln + 4 * np);
+    constexpr bool kSave = RT_PK_MARCH_SAVE && FEAT == 0 && MAXC == 1 && !MULTI && !COUNT;
+    double* s_save = kSave ? smem + pk_image_bytes(ns, np, nl) / 8 : nullptr;
     // The frame: one per launch, or frame blockIdx.z of a batch (rt_render_batch) with its own
     // camera and image source (scalar loads from the kernel arguments).
     const double* camp = P.cam_pos;
@@ -1063,6 +1183,10 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
     S.nl = nl;
     S.nb = nb;
     S.orig = nb ? s_orig : nullptr;
+    S.wstk = nullptr;
+    if constexpr ((FEAT & kFeatTris) != 0)  // after the image: 64 ints per wave
+        S.wstk = reinterpret_cast<int*>(smem + pk_image_bytes(ns, np, nl) / 8) +
+                 kPkStack * (tid >> 6);
     const int nchunks = (ns + 63) / 64;
 
     const int lane = tid & 63, wave = tid >> 6;
@@ -1120,7 +1244,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
             h.prim = 0;
             const bool hit = valid && closest_camera<MAXC, FEAT>(S, M, nchunks, cam, d, h);
             // shading inputs (Scene.h:147-154); misses carry harmless placeholders
-            const d3 hp = cam + d * h.t;
+            d3 hp = cam + d * h.t;
             // `view` is only read by the Blinn-Phong term.
             d3 view = mk(0.0, 0.0, 0.0);
             d3 inc = mk(0.0, 0.0, 0.0);
@@ -1162,7 +1286,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
                 d3 L, E;
                 pk_light_record<MAXC>(S, P, l, L, E);
                 pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, L, E, L, 0.0, bias, nchunks,
-                                            diff, spec, cnt);
+                                            diff, spec, cnt, nullptr, s_save, tid, kThreads);
             }
             if constexpr ((FEAT & kFeatArea) != 0) {
                 if (P.al_samples > 0) {
@@ -1412,8 +1536,13 @@ static void launch_packet_shape(const TraceParams& p, bool count, size_t lds, hi
     // general one
     // (a launch that records its wave durations for the tile order takes the general variant:
     // the single-sample one carries no recording code)
+    if constexpr ((FEAT & kFeatTris) != 0) lds += sizeof(int) * kPkStack * (block.x / 64);
     if (count) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, true, true, WGY>), grid, block, lds, stream, p);
-    else if (p.aa == 1 && !p.tile_cost) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, false, WGY>), grid, block, lds, stream, p);
+    else if (p.aa == 1 && !p.tile_cost)
+        hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, false, WGY>), grid, block,
+                           lds + ((RT_PK_MARCH_SAVE && FEAT == 0 && MAXC == 1)
+                                      ? sizeof(double) * kPkSaveDoubles * block.x : 0),
+                           stream, p);
     else hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, true, WGY>), grid, block, lds, stream, p);
 }
 

@@ -40,11 +40,7 @@ struct Counts {
 
 // Triangle::Intersect (Shape.h:202-220), Möller–Trumbore with the reference's operation order;
 // true with t when the triangle is hit at t > 1e-6.
-__device__ __forceinline__ bool tri_hit(const double* tri, int i, d3 o, d3 d, double& t) {
-    const double* q = tri + kTriStride * i;
-    const d3 a0 = mk(q[0], q[1], q[2]);
-    const d3 e1 = mk(q[3], q[4], q[5]);
-    const d3 e2 = mk(q[6], q[7], q[8]);
+__device__ __forceinline__ bool tri_hit_v(d3 a0, d3 e1, d3 e2, d3 o, d3 d, double& t) {
     const d3 hv = cross(d, e2);
     const double det = dot(e1, hv);
     if (det > -1e-6 && det < 1e-6) return false;
@@ -58,12 +54,17 @@ __device__ __forceinline__ bool tri_hit(const double* tri, int i, d3 o, d3 d, do
     t = f * dot(e2, qv);
     return t > 1e-6;
 }
+__device__ __forceinline__ bool tri_hit(const double* tri, int i, d3 o, d3 d, double& t) {
+    const double* q = tri + kTriStride * i;
+    return tri_hit_v(mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8]), o, d, t);
+}
 
 // Conservative ray / box test (boxes are widened at build time, rt_bvh.cpp): false only when
 // no point of the box is on the ray at t >= 0.  tn = entry parameter (a lower bound).
-__device__ __forceinline__ bool bvh_box(const double* nd, d3 o, d3 d, d3 inv, double& tn) {
+__device__ __forceinline__ bool bvh_box_v(d3 blo, d3 bhi, d3 o, d3 d, d3 inv, double& tn) {
     double lo = -INFINITY, hi = INFINITY;
     const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, ii[3] = {inv.x, inv.y, inv.z};
+    const double nd[6] = {blo.x, blo.y, blo.z, bhi.x, bhi.y, bhi.z};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         if (dd[k] != 0.0) {
@@ -81,6 +82,9 @@ __device__ __forceinline__ bool bvh_box(const double* nd, d3 o, d3 d, d3 inv, do
     }
     tn = lo;
     return !(hi < 0.0) && !(lo > hi + 1e-12 * fabs(hi));
+}
+__device__ __forceinline__ bool bvh_box(const double* nd, d3 o, d3 d, d3 inv, double& tn) {
+    return bvh_box_v(mk(nd[0], nd[1], nd[2]), mk(nd[3], nd[4], nd[5]), o, d, inv, tn);
 }
 
 // The triangles' part of IntersectClosest over the BVH.  The reference tests triangles in index
