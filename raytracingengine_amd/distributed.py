@@ -80,6 +80,52 @@ def gather_rows(tile: torch.Tensor, height: int, width: int, channels: int = 3,
     return frame
 
 
+def gather_frames(packed: torch.Tensor, nframes: int, height: int, width: int,
+                  channels: int = 3, group=None, block: int = DEFAULT_BLOCK
+                  ) -> torch.Tensor | None:
+    """A batch of frames: every rank's rows of `nframes` frames, packed frame after frame
+    (frame f at row f·rows of `packed`, the layout rt_render_batch writes), gathered to rank 0
+    with ONE gather per frame and assembled there into [nframes, height, width, channels]
+    (None elsewhere).  The layout of rt_render_gather_batch (rt_multi.cpp): frame f's gather
+    sends max_rows rows starting at row f·rows of the send buffer — the rows past this rank's
+    own are the next frame's or padding, and the assembly never reads them — and rank 0
+    receives frame f's chunks at f·n·max_rows."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    plans = [row_ranges(r, world, height, block) for r in range(world)]
+    max_rows = max(plan_rows(p) for p in plans)
+    rows = plan_rows(plans[rank])
+    if packed.shape[0] != nframes * rows:
+        raise ValueError(f"rank {rank}: {packed.shape[0]} packed rows, expected "
+                         f"{nframes} x {rows}")
+    send = torch.zeros(((nframes - 1) * rows + max_rows, width, channels), dtype=packed.dtype,
+                       device=packed.device)
+    send[: nframes * rows] = packed
+    recv = torch.empty((nframes * world * max_rows, width, channels), dtype=packed.dtype,
+                       device=packed.device) if rank == 0 else None
+    for f in range(nframes):
+        chunk = send[f * rows: f * rows + max_rows].contiguous()
+        parts = None
+        if rank == 0:
+            parts = [torch.empty_like(chunk) for _ in range(world)]
+        dist.gather(chunk, parts, dst=0, group=group)
+        if rank == 0:
+            for r in range(world):
+                base = (f * world + r) * max_rows
+                recv[base: base + max_rows] = parts[r]
+    if rank != 0:
+        return None
+    frames = torch.empty((nframes, height, width, channels), dtype=packed.dtype,
+                         device=packed.device)
+    for f in range(nframes):
+        for r in range(world):
+            k = (f * world + r) * max_rows
+            for a, b in plans[r]:
+                frames[f, a:b] = recv[k: k + (b - a)]
+                k += b - a
+    return frames
+
+
 def render_frame_tiled(render_rows: Callable[[list[tuple[int, int]]], torch.Tensor],
                        height: int, width: int, channels: int = 3, group=None,
                        block: int = DEFAULT_BLOCK) -> torch.Tensor | None:

@@ -58,6 +58,60 @@ def test_tiled_gather_equals_full_frame(tmp_path, world, name, w, h, block):
     assert np.array_equal(frame, full)
 
 
+def _batch_worker(rank, world, port, name, w, h, outdir, block, nframes):
+    import dataclasses
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import pyoracle as po
+    from raytracingengine_amd.configs import make_config
+    from raytracingengine_amd.distributed import gather_frames
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = make_config(name, w, h)
+    ranges = row_ranges(rank, world, h, block)
+    parts = []
+    for f in range(nframes):  # this rank's rows of frame f (camera f), packed frame by frame
+        cam = dataclasses.replace(sc.camera, position=_batch_position(sc, f))
+        scf = dataclasses.replace(sc, camera=cam)
+        parts += [po.render(scf, rows=(r0, r1), nthreads=1)[0] for r0, r1 in ranges]
+    packed = torch.from_numpy(np.concatenate(parts)) if parts else \
+        torch.empty((0, w, 3), dtype=torch.float64)
+    frames = gather_frames(packed, nframes, h, w, block=block)
+    if rank == 0:
+        np.save(os.path.join(outdir, "frames.npy"), frames.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _batch_position(sc, f):
+    x, y, z = sc.camera.position
+    return (x + 0.25 * f, y - 0.125 * f, z + 0.5 * f)
+
+
+@pytest.mark.parametrize("world,name,w,h,block,nframes", [(2, "c2", 64, 40, 16, 3),
+                                                          (3, "c2", 48, 37, 8, 2),
+                                                          # rank 2 owns no rows
+                                                          (3, "c2", 40, 24, 16, 2)])
+def test_batched_gather_equals_full_frames(tmp_path, world, name, w, h, block, nframes):
+    """A batch of frames (one camera each) split over the ranks, one gather per frame with the
+    send / receive layout of rt_render_gather_batch (padded chunks that overlap the next frame's
+    rows): rank 0's frames equal the single-process frames."""
+    import dataclasses
+    from oracle import pyoracle as po
+    from raytracingengine_amd.configs import make_config
+    mp.start_processes(_batch_worker,
+                       args=(world, _free_port(), name, w, h, str(tmp_path), block, nframes),
+                       nprocs=world, join=True, start_method="spawn")
+    frames = np.load(tmp_path / "frames.npy")
+    sc = make_config(name, w, h)
+    for f in range(nframes):
+        cam = dataclasses.replace(sc.camera, position=_batch_position(sc, f))
+        full, _, _ = po.render(dataclasses.replace(sc, camera=cam))
+        assert np.array_equal(frames[f], full), f
+
+
 def test_row_tile_partition():
     for H in (1, 7, 54, 1080, 4320):
         for world in (1, 2, 3, 4, 8):
