@@ -11,7 +11,7 @@ Contract (driver):  python bench.py --gpus N --steps K --warmup W
     bytes into its send buffer), ONE ncclGather per frame moves the bytes to rank 0 over xGMI,
     and rank 0 writes them into image order (rt_render_gather_batch).  At N=1 the one rank's
     rows are the frame: it renders straight into the frame buffers, nothing to gather.
-  * Frames go in batches of --batch (default 8) per call: one render launch per batch (one
+  * Frames go in batches of --batch (default 16) per call: one render launch per batch (one
     grid plane per frame, so a small per-rank share of a frame does not pay a whole launch's
     ramp and drain), the batch's ncclGathers in one ncclGroup, one assembly launch; two
     batches in flight (RT_FLAG_PIPELINE: batch b's gather overlaps batch b+1's render).
@@ -53,7 +53,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=20, help="untimed frames after the clock warm-up")
     ap.add_argument("--config", default="c2",
                     help="c1..c5 (BASELINE configs), mirror, glass, mesh, bigmesh; default c2")
-    ap.add_argument("--batch", type=int, default=8,
+    ap.add_argument("--batch", type=int, default=16,
                     help="frames per rt_render_gather_batch call (1..16 per launch)")
     ap.add_argument("--tonemap", default="reinhard_simple",
                     help="fused LDR operator (the gathered bytes)")
@@ -445,7 +445,8 @@ def main(argv=None):
     render_ms = r0[0]
     bytes_per_frame = int(r0[3]) * W * (HDR_BYTES[args.hdr] + 3)
     achieved = bytes_per_frame / (render_ms / 1e3) / 1e9 if render_ms > 0 else 0.0
-    traffic, traffic_src = load_profile(f"pmc_{args.config}_frames.json")
+    # PMC traffic of the batch launch (tools/pmc_passes.sh with the bench's batch), per launch
+    traffic, traffic_src = load_profile(f"pmc_{args.config}_batch{batch}.json")
     valu, valu_src = load_profile(f"r04_{args.config}_valu.json")
     if valu is None:
         valu, valu_src = load_profile(f"r03_{args.config}_valu.json")

@@ -73,13 +73,6 @@ constexpr int kFeatNoPL = 32;
 // Waves per SIMD of the single-sample variant for <= 64 spheres, point lights and no other
 // feature (C2): 6 with its light records read through the scalar cache (80 VGPRs, 48 B/lane of
 // scratch): C2 48.1 -> 46.7 us against 5 waves (95 VGPRs + 20 B, lights from LDS), MI355X
-// The single-sample lean variant (C2) parks the hit point, normal and diffuse sum of its lanes
-// in LDS while a wave runs the (rare) exact shadow march, so that the march's registers do not
-// force spills on the common path (RT_PK_MARCH_SAVE: 0 off, 1 on).
-#ifndef RT_PK_MARCH_SAVE
-#define RT_PK_MARCH_SAVE 0
-#endif
-constexpr int kPkSaveDoubles = 9;  // per lane: hp, n, diff
 constexpr int kPkStack = 64;       // wave-coherent BVH walk: node stack entries per wave (depth ≤ 48)
 #ifndef RT_PACKET_SMALL_WAVES
 #define RT_PACKET_SMALL_WAVES 6
@@ -103,9 +96,10 @@ constexpr int kPkStack = 64;       // wave-coherent BVH walk: node stack entries
 
 // This lane's index in the wave, formed where it is used: an opaque (volatile) mbcnt pair the
 // compiler cannot hoist and keep live — it spilled the hoisted lane·80 LDS offset of the culls
-// in the C2 variant (RT_PK_OPAQUE_LANE: 0 threadIdx.x & 63, 1 opaque).
+// in the C2 variant.  C2 46.9 → 46.5 µs per launch, interleaved 3 rounds
+// (profiles/r04_ab_c2_march_save_opaque_lane.txt; RT_PK_OPAQUE_LANE=0: threadIdx.x & 63).
 #ifndef RT_PK_OPAQUE_LANE
-#define RT_PK_OPAQUE_LANE 0
+#define RT_PK_OPAQUE_LANE 1
 #endif
 __device__ __forceinline__ int cull_lane() {
 #if RT_PK_OPAQUE_LANE
@@ -831,11 +825,10 @@ __device__ __forceinline__ Masks<MAXC> shadow_masks(const PacketScene& S, bool c
 // One light of directLightning (Scene.h:86-124) for the whole wave: every lane calls it
 // (uniform control flow for the packet reductions); `active` lanes shade.
 template <int MAXC, int FEAT, bool COUNT>
-__device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3& P, d3& n, d3 view,
+__device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P, d3 n, d3 view,
                                          const PkHit& h, d3 lpos, d3 E, d3 lcenter, double lrad,
                                          double bias, int nchunks, d3& diff, d3& spec,
-                                         Counts& cnt, const Masks<MAXC>* pre = nullptr,
-                                         double* save = nullptr, int tid = 0, int nthr = 0) {
+                                         Counts& cnt, const Masks<MAXC>* pre = nullptr) {
     double dist = 0.0, inv_d2 = 0.0;
     d3 L = mk(0.0, 0.0, 0.0);
     if (active) light_dir(lpos - P, dist, L, inv_d2);  // skipped by waves with no hit lane
@@ -931,30 +924,7 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3& 
             for (int c = 0; c < MAXC; ++c) Mu.m[c] &= t.m[c];
             Mu.pm &= t.pm;
         }
-        // `save`: this lane's hit point, normal and diffuse sum go to LDS (structure of arrays,
-        // conflict-free) for the march and come back after it; the empty asm keeps the compiler
-        // from forwarding the stored values, so their registers are free inside the march
-        if (save) {
-            double* q = save + tid;
-            q[0 * nthr] = P.x;
-            q[1 * nthr] = P.y;
-            q[2 * nthr] = P.z;
-            q[3 * nthr] = n.x;
-            q[4 * nthr] = n.y;
-            q[5 * nthr] = n.z;
-            q[6 * nthr] = diff.x;
-            q[7 * nthr] = diff.y;
-            q[8 * nthr] = diff.z;
-            __asm__ volatile("" ::: "memory");
-        }
         if (undecided) T = pk_transmittance<MAXC, FEAT>(S, Mu, nchunks, so, L, dist - bias, bias);
-        if (save) {
-            __asm__ volatile("" ::: "memory");
-            const double* q = save + tid;
-            P = mk(q[0 * nthr], q[1 * nthr], q[2 * nthr]);
-            n = mk(q[3 * nthr], q[4 * nthr], q[5 * nthr]);
-            diff = mk(q[6 * nthr], q[7 * nthr], q[8 * nthr]);
-        }
     }
     if (!need) return;
     if (COUNT) cnt.shadow++;
@@ -1101,8 +1071,6 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
     double* s_lt = s_pl + kPlStride * np;
     double* s_pln = s_lt + kLtStride * nl;                        // 4·np doubles
     const int32_t* s_orig = reinterpret_cast<const int32_t*>(s_pln + 4 * np);
-    constexpr bool kSave = RT_PK_MARCH_SAVE && FEAT == 0 && MAXC == 1 && !MULTI && !COUNT;
-    double* s_save = kSave ? smem + pk_image_bytes(ns, np, nl) / 8 : nullptr;
     // The frame: one per launch, or frame blockIdx.z of a batch (rt_render_batch) with its own
     // camera and image source (scalar loads from the kernel arguments).
     const double* camp = P.cam_pos;
@@ -1244,7 +1212,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
             h.prim = 0;
             const bool hit = valid && closest_camera<MAXC, FEAT>(S, M, nchunks, cam, d, h);
             // shading inputs (Scene.h:147-154); misses carry harmless placeholders
-            d3 hp = cam + d * h.t;
+            const d3 hp = cam + d * h.t;
             // `view` is only read by the Blinn-Phong term.
             d3 view = mk(0.0, 0.0, 0.0);
             d3 inc = mk(0.0, 0.0, 0.0);
@@ -1286,7 +1254,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
                 d3 L, E;
                 pk_light_record<MAXC>(S, P, l, L, E);
                 pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, L, E, L, 0.0, bias, nchunks,
-                                            diff, spec, cnt, nullptr, s_save, tid, kThreads);
+                                            diff, spec, cnt);
             }
             if constexpr ((FEAT & kFeatArea) != 0) {
                 if (P.al_samples > 0) {
@@ -1538,11 +1506,7 @@ static void launch_packet_shape(const TraceParams& p, bool count, size_t lds, hi
     // the single-sample one carries no recording code)
     if constexpr ((FEAT & kFeatTris) != 0) lds += sizeof(int) * kPkStack * (block.x / 64);
     if (count) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, true, true, WGY>), grid, block, lds, stream, p);
-    else if (p.aa == 1 && !p.tile_cost)
-        hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, false, WGY>), grid, block,
-                           lds + ((RT_PK_MARCH_SAVE && FEAT == 0 && MAXC == 1)
-                                      ? sizeof(double) * kPkSaveDoubles * block.x : 0),
-                           stream, p);
+    else if (p.aa == 1 && !p.tile_cost) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, false, WGY>), grid, block, lds, stream, p);
     else hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, true, WGY>), grid, block, lds, stream, p);
 }
 

@@ -2,7 +2,7 @@
 # Dev tool: rocprofv3 counter passes (one --pmc group per run) over tools/profile_kernel.py.
 # usage: tools/pmc_passes.sh <outdir> <config> [reps] [flags]
 set -e
-OUT=$1; CFG=$2; REPS=${3:-10}; FLAGS=${4:-0}
+OUT=$1; CFG=$2; REPS=${3:-10}; FLAGS=${4:-0}; BATCH=${5:-1}
 mkdir -p $OUT
 export TMPDIR=/tmp
 P=0
@@ -12,6 +12,6 @@ for grp in \
   "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_CVT GRBM_GUI_ACTIVE" \
   "FETCH_SIZE" "WRITE_SIZE"; do
   P=$((P+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$P -o pmc -- python3 tools/profile_kernel.py $CFG $REPS $FLAGS > $OUT/p$P.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$P -o pmc -- python3 tools/profile_kernel.py $CFG $REPS $FLAGS $BATCH > $OUT/p$P.log 2>&1
 done
 python3 tools/pmc_summary.py $OUT
