@@ -6,8 +6,9 @@ in KiB; on gfx950 FETCH_SIZE tallies 128-B requests at 64 B, so it is doubled; W
 taken as is."""
 import json, sys
 src, dst, config, alg = sys.argv[1], sys.argv[2], sys.argv[3], float(sys.argv[4])
+sub = sys.argv[5] if len(sys.argv) > 5 else None  # kernel name substring (several variants ran)
 d = json.load(open(src))
-k = [n for n in d if "packet_direct_kernel" in n or "trace_kernel" in n]
+k = [n for n in d if (sub in n if sub else ("packet_direct_kernel" in n or "trace_kernel" in n))]
 assert len(k) == 1, k
 c = d[k[0]]
 fetch = c["FETCH_SIZE"] * 1024 * 2
