@@ -414,7 +414,7 @@ __device__ __forceinline__ Mat load_mat(const double* m) {
 
 // One iteration of directLightning's light loop (Scene.h:86-124).  E = color*intensity.
 template <bool COUNT, bool OPQ>
-__device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 view, const Mat& m,
+__device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 view, const double* m,
                                            d3 lpos, d3 E, double bias, d3& diff, d3& spec,
                                            Counts& cnt) {
     double dist, inv_d2;
@@ -434,11 +434,11 @@ __device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 vi
     }
     if (T <= bias) return;
     diff = diff + ((E * inv_d2) * ndl) * T;
-    if (m.transparency <= 0.0 && m.specular > 0.0) {
+    if (m[5] <= 0.0 && m[4] > 0.0) {  // transparency, specular
         const d3 H = unit(L + view);
         const double ndh = smax(0.0, dot(n, H));
         if (ndh > 0.0) {
-            const double sf = pow_bp(ndh, m.shininess);
+            const double sf = pow_bp(ndh, m[3]);  // shininess
             spec = spec + ((E * inv_d2) * sf) * T;
         }
     }
@@ -447,7 +447,7 @@ __device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 vi
 // Scene::directLightning (Scene.h:79-129), plus the build-defined area-light samples.
 template <bool COUNT, bool OPQ>
 __device__ __forceinline__ d3 direct(const SceneView& S, const TraceParams& P, d3 hp, d3 view,
-                                     d3 n_in, const Mat& m, uint64_t pix, uint32_t sample,
+                                     d3 n_in, const double* m, uint64_t pix, uint32_t sample,
                                      int depth, Counts& cnt) {
     const double bias = P.bias;
     const d3 n = unit(n_in);
@@ -475,7 +475,7 @@ __device__ __forceinline__ d3 direct(const SceneView& S, const TraceParams& P, d
         }
     }
 #endif
-    return hmul(m.color, diff) + spec * m.specular;
+    return hmul(mk(m[0], m[1], m[2]), diff) + spec * m[4];
 }
 
 // What one TraceRay invocation yields before its children are traced.
@@ -488,9 +488,13 @@ struct Node {
     bool hit, refl, refr;
 };
 
+// `save` (the breadth-first level kernel, RT_WF_SAVE): this lane's hit point, shading normal and
+// incident direction are parked in LDS (structure of arrays, stride nthr) across the light loop
+// and read back for the child rays, so that their registers are free while the shadow rays run.
 template <bool TREE, bool COUNT>
 __device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, d3 o, d3 d,
-                                      uint64_t pix, uint32_t sample, int depth, Counts& cnt) {
+                                      uint64_t pix, uint32_t sample, int depth, Counts& cnt,
+                                      double* save = nullptr, int nthr = 0) {
     Node nd;
     nd.refl = false;
     nd.refr = false;
@@ -505,33 +509,54 @@ __device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, 
     const double bias = P.bias;
     const d3 hp = o + d * h.t;  // Rayon::pointAtDistance
     const d3 gn = normal_of(S, h, hp);
-    const Mat m = load_mat(material_of(S, h));
+    // the material record (r g b shininess specular transparency ior), read at each use: a
+    // copy of all seven values stayed live across the light loop (14 VGPRs)
+    const double* m = material_of(S, h);
     const d3 inc = unit(d);
     const bool front = dot(gn, inc) < 0.0;
     const d3 n = front ? gn : -gn;
     const d3 view = -inc;
-    const double tr = sclamp(m.transparency, 0.0, 1.0);
+    const double tr = sclamp(m[5], 0.0, 1.0);
+    if (save) {
+        save[0 * nthr] = hp.x;
+        save[1 * nthr] = hp.y;
+        save[2 * nthr] = hp.z;
+        save[3 * nthr] = n.x;
+        save[4 * nthr] = n.y;
+        save[5 * nthr] = n.z;
+        save[6 * nthr] = inc.x;
+        save[7 * nthr] = inc.y;
+        save[8 * nthr] = inc.z;
+        __asm__ volatile("" ::: "memory");  // no forwarding of the stored values
+    }
     const d3 local = direct<COUNT, !TREE>(S, P, hp, view, n, m, pix, sample, depth, cnt);
+    d3 hp_c = hp, n_c = n, inc_c = inc;  // the values the child rays start from
+    if (save) {
+        __asm__ volatile("" ::: "memory");
+        hp_c = mk(save[0 * nthr], save[1 * nthr], save[2 * nthr]);
+        n_c = mk(save[3 * nthr], save[4 * nthr], save[5 * nthr]);
+        inc_c = mk(save[6 * nthr], save[7 * nthr], save[8 * nthr]);
+    }
     d3 fin = mk(0.0, 0.0, 0.0);
     if (tr < 1.0) fin = fin + local * (1.0 - tr);
     nd.value = fin;
-    double refl_w = m.specular;
+    double refl_w = m[4];
     if (TREE && tr > 0.0) {
         // fresnel (Scene.h:26-28, 161-164); only consumed when tr > 0.
-        const double cos_t = smax(0.0, dot(n, view));
-        const double eta_t = m.ior;
+        const double cos_t = smax(0.0, dot(n_c, -inc_c));
+        const double eta_t = m[6];
         const double r0 = (eta_t - 1.0) / (eta_t + 1.0);
         const double f0 = r0 * r0;  // pow(x, 2.0)
         // pow(1 - cosθ, 5) through pow_bp (rt_device.hpp: ≤ 2e-16 absolute on [0, 1], the
         // libm pow out of line outside (0, 1.5)) instead of the inlined libm pow
         double F = f0 + (1.0 - f0) * pow_bp(1.0 - cos_t, 5.0);
         const double eta = front ? (1.0 / eta_t) : (eta_t / 1.0);
-        d3 rd = refract(inc, n, eta);
+        d3 rd = refract(inc_c, n_c, eta);
         if (length(rd) > bias) {
             rd = unit(rd);
             nd.refr = true;
             nd.fd = rd;
-            nd.fo = hp + rd * (bias * 1e2);
+            nd.fo = hp_c + rd * (bias * 1e2);
             nd.fw = tr * (1.0 - F);
         } else {
             F = 1.0;
@@ -539,10 +564,10 @@ __device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, 
         refl_w = F;
     }
     if (refl_w > bias) {
-        const d3 R = unit(reflect(inc, n));
+        const d3 R = unit(reflect(inc_c, n_c));
         nd.refl = true;
         nd.rd = R;
-        nd.ro = hp + R * bias;
+        nd.ro = hp_c + R * bias;
         nd.rw = refl_w;
     }
     return nd;

@@ -69,9 +69,22 @@ __device__ __forceinline__ uint32_t wf_tile_order(const TraceParams& P, uint32_t
     return (yl * P.width + x) * aa + s;
 }
 
-// level kernels: 2 waves/SIMD, 3 in the lean build (213 → 168 VGPRs: glass 1.58 → 1.54 ms)
+// level kernels: 2 waves/SIMD, 4 in the lean build (213 → 168 VGPRs: glass 1.58 → 1.54 ms at 3;
+// round 4: shade()'s material read at each use and its hit point / normal / direction parked in
+// LDS across the light loop (RT_WF_SAVE) → 128 VGPRs at 4 waves/SIMD: glass 975 → 964 µs,
+// profiles/r04_ab_glass_level_save.txt)
+#ifndef RT_WF_SAVE
 #ifdef RT_LEAN_GENERIC
-constexpr int kWfLevelWaves = 3;
+#define RT_WF_SAVE 1
+#else
+#define RT_WF_SAVE 0
+#endif
+#endif
+#ifdef RT_LEAN_GENERIC
+#ifndef RT_WF_LEVEL_WAVES
+#define RT_WF_LEVEL_WAVES 4
+#endif
+constexpr int kWfLevelWaves = RT_WF_LEVEL_WAVES;
 #else
 constexpr int kWfLevelWaves = 2;
 #endif
@@ -80,6 +93,12 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
                                                                              WfArena A, int level) {
     extern __shared__ double smem[];
     const SceneView S = stage_scene<LDS>(P, smem, threadIdx.x, kWfThreads);
+#if RT_WF_SAVE
+    __shared__ double s_save[9 * kWfThreads];  // shade()'s parked hit point, normal, direction
+    double* const save = s_save + threadIdx.x;
+#else
+    double* const save = nullptr;
+#endif
     uint32_t base, n;
     level_range(A, level, base, n);
     const uint32_t next = base + n;  // first node id of level + 1
@@ -136,7 +155,7 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
         nd.rw = 0.0;
         if (active) {
             if (level >= P.max_rec) nd.value = sky(d);  // TraceRay at depth >= maxRecursion
-            else nd = shade<TREE, false>(S, P, o, d, pix, sample, level, cnt);
+            else nd = shade<TREE, false>(S, P, o, d, pix, sample, level, cnt, save, kWfThreads);
         }
         const bool want_f = active && TREE && nd.hit && nd.refr;
         const bool want_r = active && nd.hit && nd.refl;
