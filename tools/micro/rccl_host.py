@@ -53,6 +53,38 @@ e1.record(s)
 torch.cuda.synchronize()
 print({"bytes": nbytes, "host_us_per_gather": round(host, 2),
        "stream_us_per_gather": round(e0.elapsed_time(e1) / iters * 1e3, 2)})
+# a batch: 16 gathers in one group (rt_render_gather_batch) vs one gather of 16x the bytes
+big_src = torch.empty(16 * nbytes, dtype=torch.uint8, device="cuda")
+big_dst = torch.empty(16 * nbytes, dtype=torch.uint8, device="cuda")
+
+
+def group16():
+    lib.ncclGroupStart()
+    for f in range(16):
+        lib.ncclGather(big_src.data_ptr() + f * nbytes, big_dst.data_ptr() + f * nbytes, nbytes,
+                       0, 0, comm, st)
+    lib.ncclGroupEnd()
+
+
+def one_big():
+    lib.ncclGroupStart()
+    lib.ncclGather(big_src.data_ptr(), big_dst.data_ptr(), 16 * nbytes, 0, 0, comm, st)
+    lib.ncclGroupEnd()
+
+
+for fn, name in ((group16, "group_of_16_gathers"), (one_big, "one_gather_of_16x")):
+    for _ in range(20):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(s)
+    for _ in range(200):
+        fn()
+    e1.record(s)
+    host = (time.perf_counter() - t0) / 200 * 1e6
+    torch.cuda.synchronize()
+    print({name: {"host_us_per_call": round(host, 2),
+                  "stream_us_per_call": round(e0.elapsed_time(e1) / 200 * 1e3, 2)}})
 # the empty ctypes call, for scale
 t0 = time.perf_counter()
 for _ in range(iters):
