@@ -382,17 +382,6 @@ rt_status scratch_done(rt_context* ctx) {
     return RT_OK;
 }
 
-bool render_uses_context_scratch(const rt_scene* sc, const rt_render_opts* opts) {
-    rt_render_opts o;
-    if (opts) o = *opts;
-    else rt_render_opts_default(&o);
-    if (o.flags & RT_FLAG_COUNT_RAYS) return true;  // the context's counter buffer
-    int path = kPathDirect;
-    if (sc->any_transparent) path = kPathTree;
-    else if (!(sc->max_specular <= o.bias) && o.max_recursion >= 1) path = kPathChain;
-    return uses_wavefront_arena(path, o.flags);
-}
-
 rt_status check_batch(const rt_camera* cams, int nframes) {
     if (!cams || nframes < 1) return fail(RT_ERR_INVALID_ARG, "frame batch: no cameras");
     for (int f = 0; f < nframes; ++f) {

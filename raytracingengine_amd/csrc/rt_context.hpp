@@ -149,10 +149,9 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
 rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* cams, int nframes,
                          const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr);
 rt_status check_batch(const rt_camera* cams, int nframes);
-// Whether a render uses scratch the context holds once (the breadth-first TraceRay arena, the
-// ray counters): frames on different streams that do must not overlap (rt_queue.cpp).
+// Whether a render takes the breadth-first TraceRay path, whose arena is one per context (as are
+// the ray counters): renders that use them are ordered across streams (scratch_wait/_done).
 bool uses_wavefront_arena(int path, int flags);
-bool render_uses_context_scratch(const rt_scene* sc, const rt_render_opts* opts);
 // Orders work on ctx->stream after the last render that used the context's scratch (any
 // stream), and marks ctx->stream's work so far as the latest such user.
 rt_status scratch_wait(rt_context* ctx);

@@ -179,3 +179,42 @@ def test_queue_refraction_tree_frames_share_the_arena_safely(ctx, depth):
         q.close()
         glass.close()
         c2.close()
+
+
+def test_arena_shared_by_queue_and_context_stream(ctx):
+    """The breadth-first arena is one per context: a refraction-tree render on the context's own
+    stream (rt_render_device) between queued ones on other streams is ordered behind them and
+    they behind it (rt_capi.cpp scratch_wait / scratch_done), whatever API enqueued each render.
+    Every frame equals its synchronous render."""
+    glass = ctx.scene(make_config("glass", 240, 135))
+    q = capi.Queue(ctx, 2)
+    W, H = 240, 135
+    base = glass.camera["position"][0].copy()
+    cams = [base, base + (0.5, 0.25, 1.5), base + (-0.5, 0.0, 0.75)]
+    try:
+        ref = []
+        for c in cams:
+            glass.camera["position"][0] = c
+            ref.append(glass.render(hdr64=True, tonemap=1))
+        opts = capi.default_opts(tonemap=1)
+        bufs, kinds = [], []
+        for i in range(9):
+            k = i % 3
+            glass.camera["position"][0] = cams[k]
+            h = torch.empty(H * W * 3, dtype=torch.float64, device="cuda")
+            l = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")
+            if k == 2:
+                glass.render_device(h.data_ptr(), None, l.data_ptr(), opts)  # context stream
+            else:
+                q.submit(glass, opts, h.data_ptr(), None, l.data_ptr())
+            bufs.append((h, l))
+            kinds.append(k)
+        q.synchronize()
+        ctx.synchronize()
+        for i, (h, l) in enumerate(bufs):
+            assert np.array_equal(h.cpu().numpy().reshape(H, W, 3), ref[kinds[i]]["hdr64"]), i
+            assert np.array_equal(l.cpu().numpy().reshape(H, W, 3), ref[kinds[i]]["ldr"]), i
+    finally:
+        glass.camera["position"][0] = base
+        q.close()
+        glass.close()
