@@ -270,11 +270,12 @@ class Runner:
             self.ctx.reset_stats()
         return st.trace_rays + st.shadow_rays
 
-    def rank_plan(self, H, block):
-        """rt_render_opts of this rank's block-cyclic rows (its share of every frame)."""
+    def rank_plan(self, H, block, rank=None):
+        """rt_render_opts of a rank's block-cyclic rows (its share of every frame; this rank's
+        by default)."""
         o = self.capi.default_opts(tonemap=-1)
         if self.world > 1:
-            o.row_begin, o.row_end = self.rank * block, H
+            o.row_begin, o.row_end = (self.rank if rank is None else rank) * block, H
             o.row_block, o.row_cycle = block, self.world
         return o
 
@@ -293,11 +294,14 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     split = gather and R.world > 1
     plan = R.rank_plan(H, block) if split else capi.default_opts(tonemap=-1)
     rows = capi.rendered_rows(plan, H) if plan.row_begin < H else 0
+    # rt_render_gather_batch lays every rank's frames max_rows rows apart (the largest rank's)
+    max_rows = max(capi.rendered_rows(R.rank_plan(H, block, r), H) for r in range(R.world)
+                   if r * block < H) if split else rows
     rays_rank = R.count_rays(dscene, plan) if rows else 0
     comm = R.comm if split else R.solo_comm()
     # two sets of buffers (the pipelined slots): batch b writes set b mod 2
     hdr_dtype = torch.float64 if hdr == "f64" else torch.float32
-    local = [torch.empty(max(rows, 1) * W * 3 * batch, dtype=hdr_dtype, device="cuda")
+    local = [torch.empty(max(max_rows, 1) * W * 3 * batch, dtype=hdr_dtype, device="cuda")
              for _ in range(2)]
     root = R.rank == 0 or not split
     ldr = [torch.empty(H * W * 3 * batch if root else 1, dtype=torch.uint8, device="cuda")

@@ -280,13 +280,15 @@ rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, i
                                void* d_hdr64, void* d_hdr32, void* d_ldr);
 /* A batch of nframes frames (see rt_render_batch: one camera per frame, same width / height /
  * focal / aa_samples) in one call: this rank renders its rows of every frame in one launch,
- * then ONE ncclGather per frame and gathered output — all of them in one ncclGroup, so a batch
- * costs one RCCL launch — and rank 0 assembles every frame (one launch).  On rank 0 the d_* hold
- * nframes whole frames back to back (frame f at f*W*H*3 elements).  rank_* (any may be NULL)
- * receive outputs that are rendered but NOT gathered: this rank's rows of every frame, packed
- * (frame f at f*rows*W*3, rows = rt_gather_timing.rows) — e.g. the float64 HDR framebuffer
- * kept where it was rendered while the tonemapped bytes are gathered.  An output is either
- * gathered (in `outputs`) or rank-local, not both.  rt_render_gather = nframes 1, no rank_*. */
+ * frame after frame at a stride of max_rows rows (the largest rank's row count), then ONE
+ * ncclGather per gathered output moves the whole batch, and rank 0 assembles every frame (one
+ * launch).  On rank 0 the d_* hold nframes whole frames back to back (frame f at f*W*H*3
+ * elements).  rank_* (any may be NULL) receive outputs that are rendered but NOT gathered: this
+ * rank's rows of every frame, packed, frame f at f*max_rows*W*3 elements (max_rows =
+ * rt_gather_timing.max_rows; a rank with fewer rows leaves the rest of each frame's stride
+ * unwritten; buffers of nframes*max_rows*W*3 elements) — e.g. the float64 HDR framebuffer kept
+ * where it was rendered while the tonemapped bytes are gathered.  An output is either gathered
+ * (in `outputs`) or rank-local, not both.  rt_render_gather = nframes 1, no rank_*. */
 rt_status rt_render_gather_batch(rt_comm* comm, const rt_scene* scene, const rt_camera* cams,
                                  int nframes, const rt_render_opts* opts, int outputs,
                                  void* d_hdr64, void* d_hdr32, void* d_ldr, void* rank_hdr64,

@@ -521,9 +521,9 @@ class Comm:
                             outputs: int, d_hdr64: int | None = None, d_hdr32: int | None = None,
                             d_ldr: int | None = None, rank_hdr64: int | None = None,
                             rank_hdr32: int | None = None, rank_ldr: int | None = None):
-        """Collective: len(cams) frames, this rank's rows of each in one launch, one gather per
-        frame and output in one RCCL group, rank 0 assembles (rt_render_gather_batch);
-        rank_* receive outputs rendered but not gathered (this rank's rows)."""
+        """Collective: len(cams) frames, this rank's rows of each in one launch, one gather of
+        the whole batch per output, rank 0 assembles (rt_render_gather_batch); rank_* receive
+        outputs rendered but not gathered (this rank's rows, frames max_rows rows apart)."""
         cams = np.ascontiguousarray(cams)
         _check(_lib.rt_render_gather_batch(self._h, dscene._h, cams.ctypes.data, len(cams),
                                            ctypes.byref(opts), outputs, d_hdr64, d_hdr32, d_ldr,

@@ -1,6 +1,7 @@
-// rt_assemble.hip — rank 0's step of a row-tiled multi-GPU frame (rt_multi.cpp): the gathered
-// per-rank buffers [n][max_rows][row_bytes] (each rank's block-cyclic rows, packed in render
-// order) are written into image row order.  Pure data movement, HBM bound: each image row is
+// rt_assemble.hip — rank 0's step of a row-tiled multi-GPU frame batch (rt_multi.cpp): the
+// gathered per-rank buffers [n][frames][max_rows][row_bytes] (each rank's block-cyclic rows of
+// every frame, packed in render order, one ncclGather of the whole batch) are written into image
+// row order, frame after frame.  Pure data movement, HBM bound: each image row is
 // read once and written once, 16 B per lane where the row pitch allows.
 #include <hip/hip_runtime.h>
 
@@ -12,14 +13,15 @@ namespace rtamd {
 
 namespace {
 
-// Source row (in the gathered buffer) of image row y: block b = y / B belongs to rank b % n,
-// as its (b / n)-th block (rt_render_opts row_block / row_cycle with row_begin = rank*B).
-__device__ __forceinline__ size_t gathered_row(uint32_t y, uint32_t block, uint32_t n,
-                                               uint32_t max_rows) {
+// Source row (in the gathered buffer) of frame z's image row y: block b = y / B belongs to rank
+// b % n, as its (b / n)-th block (rt_render_opts row_block / row_cycle with row_begin = rank*B),
+// in that rank's frame z.
+__device__ __forceinline__ size_t gathered_row(uint32_t y, uint32_t z, uint32_t frames,
+                                               uint32_t block, uint32_t n, uint32_t max_rows) {
     const uint32_t b = y / block;
     const uint32_t rank = b % n;
     const uint32_t local = (b / n) * block + (y - b * block);
-    return static_cast<size_t>(rank) * max_rows + local;
+    return (static_cast<size_t>(rank) * frames + z) * max_rows + local;
 }
 
 template <typename V>
@@ -28,12 +30,12 @@ __global__ __launch_bounds__(256) void assemble_rows_kernel(const V* __restrict_
                                                             uint32_t words_per_row,
                                                             uint32_t height, uint32_t block,
                                                             uint32_t n, uint32_t max_rows) {
-    // frame blockIdx.z of a batch: n·max_rows gathered rows in, height image rows out
-    src += static_cast<size_t>(blockIdx.z) * n * max_rows * words_per_row;
+    // frame blockIdx.z of a batch: height image rows out
     dst += static_cast<size_t>(blockIdx.z) * height * words_per_row;
     // one workgroup row-strip: blockIdx.y walks image rows, x covers the row's words
     for (uint32_t y = blockIdx.y; y < height; y += gridDim.y) {
-        const V* s = src + gathered_row(y, block, n, max_rows) * words_per_row;
+        const V* s =
+            src + gathered_row(y, blockIdx.z, gridDim.z, block, n, max_rows) * words_per_row;
         V* d = dst + static_cast<size_t>(y) * words_per_row;
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < words_per_row;
              i += gridDim.x * blockDim.x)

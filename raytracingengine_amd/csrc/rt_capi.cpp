@@ -402,7 +402,8 @@ rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* c
 }
 
 rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* cams, int nframes,
-                         const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr) {
+                         const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr,
+                         uint32_t frame_rows) {
     TraceParams p;
     int path;
     bool lds;
@@ -421,7 +422,9 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
     const bool packet_path = path == kPathDirect && !(flags & RT_FLAG_GENERIC_KERNEL) &&
                              p.ns <= packet_max_spheres() &&
                              packet_lds_bytes(p.ns, p.np, p.nl) <= ctx->lds_limit;
-    const size_t frame_px = static_cast<size_t>(rows) * p.width;
+    if (frame_rows && frame_rows < rows)
+        return fail(RT_ERR_INVALID_ARG, "frame batch: frame stride below the rendered rows");
+    const size_t frame_px = static_cast<size_t>(frame_rows ? frame_rows : rows) * p.width;
     if (nframes > 1 && (!packet_path || nframes > kPkMaxBatch)) {
         // one launch per frame (other kernels), or per kPkMaxBatch frames
         const int step = packet_path ? kPkMaxBatch : 1;
@@ -429,7 +432,7 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
             const size_t off = 3 * frame_px * static_cast<size_t>(f0);
             st = enqueue_frames(ctx, sc, cams + f0, std::min(step, nframes - f0), opts,
                                 d64 ? d64 + off : nullptr, d32 ? d32 + off : nullptr,
-                                dldr ? dldr + off : nullptr);
+                                dldr ? dldr + off : nullptr, frame_rows);
             if (st != RT_OK) return st;
         }
         return RT_OK;

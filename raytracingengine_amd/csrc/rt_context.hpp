@@ -144,10 +144,13 @@ rt_status validate_camera(const rt_camera* cam);
 rt_status enqueue_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
                          const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr);
 // The same for a batch of nframes cameras (same width / height / focal / aa_samples): frame f
-// writes its rows f·rows·width pixels into each output.  Packet-kernel scenes render up to
-// kPkMaxBatch frames per launch (blockIdx.z = frame), other scenes one launch per frame.
+// writes its rows f·stride·width pixels into each output, stride = frame_rows (0: the rows the
+// render produces; larger pads every frame, as the row-split gather's send buffers are laid out).
+// Packet-kernel scenes render up to kPkMaxBatch frames per launch (blockIdx.z = frame), other
+// scenes one launch per frame.
 rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* cams, int nframes,
-                         const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr);
+                         const rt_render_opts* opts, double* d64, float* d32, uint8_t* dldr,
+                         uint32_t frame_rows = 0);
 rt_status check_batch(const rt_camera* cams, int nframes);
 // Whether a render takes the breadth-first TraceRay path, whose arena is one per context (as are
 // the ray counters): renders that use them are ordered across streams (scratch_wait/_done).

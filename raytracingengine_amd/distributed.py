@@ -83,45 +83,40 @@ def gather_rows(tile: torch.Tensor, height: int, width: int, channels: int = 3,
 def gather_frames(packed: torch.Tensor, nframes: int, height: int, width: int,
                   channels: int = 3, group=None, block: int = DEFAULT_BLOCK
                   ) -> torch.Tensor | None:
-    """A batch of frames: every rank's rows of `nframes` frames, packed frame after frame
-    (frame f at row f·rows of `packed`, the layout rt_render_batch writes), gathered to rank 0
-    with ONE gather per frame and assembled there into [nframes, height, width, channels]
-    (None elsewhere).  The layout of rt_render_gather_batch (rt_multi.cpp): frame f's gather
-    sends max_rows rows starting at row f·rows of the send buffer — the rows past this rank's
-    own are the next frame's or padding, and the assembly never reads them — and rank 0
-    receives frame f's chunks at f·n·max_rows."""
+    """A batch of frames: every rank's rows of `nframes` frames gathered to rank 0 with ONE
+    gather and assembled there into [nframes, height, width, channels] (None elsewhere).  The
+    layout of rt_render_gather_batch (rt_multi.cpp): each rank's frames lie max_rows rows apart
+    (max_rows = the largest rank's row count; the rows past a rank's own are padding the
+    assembly never reads), the gather moves the rank's nframes·max_rows rows at once and rank 0
+    receives [world][nframes][max_rows] rows.  `packed` holds either that padded layout
+    (nframes·max_rows rows, what the rank-local outputs of rt_render_gather_batch hold) or the
+    frames back to back (nframes·rows rows, rt_render_batch's)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     plans = [row_ranges(r, world, height, block) for r in range(world)]
     max_rows = max(plan_rows(p) for p in plans)
     rows = plan_rows(plans[rank])
-    if packed.shape[0] != nframes * rows:
+    if packed.shape[0] == nframes * max_rows:
+        send = packed.reshape(nframes, max_rows, width, channels)
+    elif packed.shape[0] == nframes * rows:
+        send = torch.zeros((nframes, max_rows, width, channels), dtype=packed.dtype,
+                           device=packed.device)
+        send[:, :rows] = packed.reshape(nframes, rows, width, channels)
+    else:
         raise ValueError(f"rank {rank}: {packed.shape[0]} packed rows, expected "
-                         f"{nframes} x {rows}")
-    send = torch.zeros(((nframes - 1) * rows + max_rows, width, channels), dtype=packed.dtype,
-                       device=packed.device)
-    send[: nframes * rows] = packed
-    recv = torch.empty((nframes * world * max_rows, width, channels), dtype=packed.dtype,
-                       device=packed.device) if rank == 0 else None
-    for f in range(nframes):
-        chunk = send[f * rows: f * rows + max_rows].contiguous()
-        parts = None
-        if rank == 0:
-            parts = [torch.empty_like(chunk) for _ in range(world)]
-        dist.gather(chunk, parts, dst=0, group=group)
-        if rank == 0:
-            for r in range(world):
-                base = (f * world + r) * max_rows
-                recv[base: base + max_rows] = parts[r]
+                         f"{nframes} x {rows} or {nframes} x {max_rows}")
+    send = send.contiguous()
+    recv = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+    dist.gather(send, recv, dst=0, group=group)
     if rank != 0:
         return None
     frames = torch.empty((nframes, height, width, channels), dtype=packed.dtype,
                          device=packed.device)
     for f in range(nframes):
         for r in range(world):
-            k = (f * world + r) * max_rows
+            k = 0
             for a, b in plans[r]:
-                frames[f, a:b] = recv[k: k + (b - a)]
+                frames[f, a:b] = recv[r][f, k: k + (b - a)]
                 k += b - a
     return frames
 

@@ -58,7 +58,7 @@ def test_tiled_gather_equals_full_frame(tmp_path, world, name, w, h, block):
     assert np.array_equal(frame, full)
 
 
-def _batch_worker(rank, world, port, name, w, h, outdir, block, nframes):
+def _batch_worker(rank, world, port, name, w, h, outdir, block, nframes, padded):
     import dataclasses
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -78,6 +78,12 @@ def _batch_worker(rank, world, port, name, w, h, outdir, block, nframes):
         parts += [po.render(scf, rows=(r0, r1), nthreads=1)[0] for r0, r1 in ranges]
     packed = torch.from_numpy(np.concatenate(parts)) if parts else \
         torch.empty((0, w, 3), dtype=torch.float64)
+    if padded:  # the rank-local layout of rt_render_gather_batch: frames max_rows rows apart
+        rows = plan_rows(ranges)
+        max_rows = max(plan_rows(row_ranges(r, world, h, block)) for r in range(world))
+        pad = torch.full((nframes, max_rows, w, 3), float("nan"), dtype=torch.float64)
+        pad[:, :rows] = packed.reshape(nframes, rows, w, 3)
+        packed = pad.reshape(nframes * max_rows, w, 3)
     frames = gather_frames(packed, nframes, h, w, block=block)
     if rank == 0:
         np.save(os.path.join(outdir, "frames.npy"), frames.numpy())
@@ -90,19 +96,22 @@ def _batch_position(sc, f):
     return (x + 0.25 * f, y - 0.125 * f, z + 0.5 * f)
 
 
-@pytest.mark.parametrize("world,name,w,h,block,nframes", [(2, "c2", 64, 40, 16, 3),
-                                                          (3, "c2", 48, 37, 8, 2),
-                                                          # rank 2 owns no rows
-                                                          (3, "c2", 40, 24, 16, 2)])
-def test_batched_gather_equals_full_frames(tmp_path, world, name, w, h, block, nframes):
-    """A batch of frames (one camera each) split over the ranks, one gather per frame with the
-    send / receive layout of rt_render_gather_batch (padded chunks that overlap the next frame's
-    rows): rank 0's frames equal the single-process frames."""
+@pytest.mark.parametrize("world,name,w,h,block,nframes,padded", [
+    (2, "c2", 64, 40, 16, 3, False),
+    (3, "c2", 48, 37, 8, 2, True),
+    (3, "c2", 40, 24, 16, 2, False),   # rank 2 owns no rows
+    (3, "c2", 40, 24, 16, 3, True)])
+def test_batched_gather_equals_full_frames(tmp_path, world, name, w, h, block, nframes, padded):
+    """A batch of frames (one camera each) split over the ranks, ONE gather of the whole batch
+    with the send / receive layout of rt_render_gather_batch (each rank's frames max_rows rows
+    apart, NaN padding that the assembly must never read): rank 0's frames equal the
+    single-process frames."""
     import dataclasses
     from oracle import pyoracle as po
     from raytracingengine_amd.configs import make_config
     mp.start_processes(_batch_worker,
-                       args=(world, _free_port(), name, w, h, str(tmp_path), block, nframes),
+                       args=(world, _free_port(), name, w, h, str(tmp_path), block, nframes,
+                             padded),
                        nprocs=world, join=True, start_method="spawn")
     frames = np.load(tmp_path / "frames.npy")
     sc = make_config(name, w, h)

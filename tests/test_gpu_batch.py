@@ -243,9 +243,10 @@ def test_gather_batch_rejects_gathered_and_local_output(ctx, comm1):
                                                      ("c2", 200, 40, 4, 16, 2)])
 def test_gather_all_batch_local_ranks_is_the_frames(name, w, h, ranks, block, nf):
     """The multi-rank batch on one GPU through local communicators: every rank renders its
-    block-cyclic rows of every frame in one launch into a padded send buffer (frame f at f·rows,
-    max_rows sent from there), rank 0 receives frame f's chunks at f·n·max_rows and assembles
-    all frames in one launch.  Ranks with fewer rows (200x40 over 4 ranks of 16-row blocks:
+    block-cyclic rows of every frame in one launch into a padded send buffer (frame f at
+    f·max_rows), the whole batch moves in one copy per rank (ONE ncclGather on RCCL
+    communicators), rank 0 receives [n][frames][max_rows] rows and assembles all frames in one
+    launch.  Ranks with fewer rows (200x40 over 4 ranks of 16-row blocks:
     one rank has none) included.  Every frame = the single-rank frame."""
     ctxs = [capi.Context(0) for _ in range(ranks)]
     try:
