@@ -8,12 +8,12 @@ Contract (driver):  python bench.py --gpus N --steps K --warmup W
     C2 frame — Scene::RenderImage() into the float64 Vec3 framebuffer + the fused Reinhard bytes
     (RaytracingEngine.cpp:133), everything resident in HBM — split into block-cyclic 16-row
     blocks over the N ranks.  Every rank renders its rows (f64 HDR rows kept on the rank, the
-    bytes into its send buffer), ONE ncclGather per frame moves the bytes to rank 0 over xGMI,
+    bytes into its send buffer), ONE ncclGather per batch moves the bytes to rank 0 over xGMI,
     and rank 0 writes them into image order (rt_render_gather_batch).  At N=1 the one rank's
     rows are the frame: it renders straight into the frame buffers, nothing to gather.
   * Frames go in batches of --batch (default 16) per call: one render launch per batch (one
     grid plane per frame, so a small per-rank share of a frame does not pay a whole launch's
-    ramp and drain), the batch's ncclGathers in one ncclGroup, one assembly launch; two
+    ramp and drain), one ncclGather and one assembly launch per batch; two
     batches in flight (RT_FLAG_PIPELINE: batch b's gather overlaps batch b+1's render).
   * Untimed frames for --clock-warmup-ms (default 50 ms) of wall time so the GPU is at its
     sustained clock (it needs ~30 ms of load to leave idle: 143 → 45 µs per C2 frame,
@@ -285,7 +285,7 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
                  pipeline=True, event_every=4, camera_step=None, gather=True):
     """Frames of `sc` split over the ranks (block-cyclic rows), `batch` frames per
     rt_render_gather_batch call: this rank's rows of the HDR framebuffer stay on the rank, the
-    fused bytes are gathered to rank 0 (one ncclGather per frame; none at N=1) and assembled.
+    fused bytes are gathered to rank 0 (one ncclGather per batch; none at N=1) and assembled.
     gather=False: every rank renders whole frames of its own (weak scaling; same call on a
     one-rank view).  camera_step(base, frame) -> a new camera position per frame."""
     torch, capi = R.torch, R.capi
@@ -421,7 +421,7 @@ def workload_text(sc, world, block, batch, hdr, tonemap_name):
     return (f"{sc.name}: {W}x{H}, {len(sc.spheres)} spheres, {len(sc.planes)} planes, "
             f"{len(sc.lights)} point lights, AA=1, static camera; a step = one frame: every "
             f"rank renders its block-cyclic {block}-row blocks ({hdr} Vec3 HDR rows kept on the "
-            f"rank + fused {tonemap_name} u8), one ncclGather per frame moves the u8 rows to "
+            f"rank + fused {tonemap_name} u8), one ncclGather per batch moves the u8 rows to "
             f"rank 0, which assembles the frame (N=1: the one rank renders the whole frame "
             f"straight into it); {batch} frames per call")
 
@@ -467,7 +467,7 @@ def main(argv=None):
                                       args.tonemap),
             "global_batch": args.steps, "resolution": [W, H],
             "parallelism": f"block-cyclic rows ({args.row_block}-row blocks) x{R.world} + one "
-                           f"ncclGather per frame",
+                           f"ncclGather per batch of frames",
             "frames_per_call": batch, "rays_per_frame": int(res["rays"]),
         },
         "frames_per_sec": round(args.steps / elapsed, 3),
