@@ -1282,17 +1282,20 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
                         ((0.5 * (length(eu) + length(ev))) / k) * (1.0 + kCullRel) +
                         1e-12 * (fabs(corner.x) + fabs(corner.y) + fabs(corner.z) + fabs(eu.x) +
                                  fabs(eu.y) + fabs(eu.z) + fabs(ev.x) + fabs(ev.y) + fabs(ev.z));
+                    // the stratum coordinates x / k as div_core with k's refined reciprocal (the
+                    // correctly rounded quotient, rt_device.hpp: 0 ≤ x < k + 1, k ≤ 2^31)
+                    const double rk = rcp_refined(k);
                     for (int q = 0; q < P.al_samples; ++q) {
                         const double r1 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q));
                         const double r2 =
                             u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(q) + 1u);
-                        const double fu = (static_cast<double>(q % P.al_k) + r1) / k;
-                        const double fv = (static_cast<double>(q / P.al_k) + r2) / k;
+                        const double fu = div_core(static_cast<double>(q % P.al_k) + r1, k, rk);
+                        const double fv = div_core(static_cast<double>(q / P.al_k) + r2, k, rk);
                         const d3 lpos = (corner + eu * fu) + ev * fv;
                         Masks<MAXC> Mq = Ma;
                         if (per_cell) {  // uniform
-                            const double cu = (static_cast<double>(q % P.al_k) + 0.5) / k;
-                            const double cv = (static_cast<double>(q / P.al_k) + 0.5) / k;
+                            const double cu = div_core(static_cast<double>(q % P.al_k) + 0.5, k, rk);
+                            const double cv = div_core(static_cast<double>(q / P.al_k) + 0.5, k, rk);
                             const Masks<MAXC> Mc = cull_capsule<MAXC, FEAT>(
                                 S, B.c, B.R, (corner + eu * cu) + ev * cv, cell_r, bias);
 #pragma unroll
