@@ -69,20 +69,17 @@ __device__ __forceinline__ uint32_t wf_tile_order(const TraceParams& P, uint32_t
     return (yl * P.width + x) * aa + s;
 }
 
-// level kernels: 2 waves/SIMD, 4 in the lean build (213 → 168 VGPRs: glass 1.58 → 1.54 ms at 3;
-// round 4: shade()'s material read at each use and its hit point / normal / direction parked in
-// LDS across the light loop (RT_WF_SAVE) → 128 VGPRs at 4 waves/SIMD: glass 975 → 964 µs,
-// profiles/r04_ab_glass_level_save.txt)
+// level kernels: 2 waves/SIMD, 3 in the lean build (213 → 168 VGPRs: glass 1.58 → 1.54 ms).
+// RT_WF_SAVE=1 RT_WF_LEVEL_WAVES=4 (shade()'s hit point / normal / direction parked in LDS across
+// the light loop: 128 VGPRs at 4 waves/SIMD) renders glass 1.2 % faster (964 vs 975 µs) but
+// spills 144-160 B/lane, which costs 1.08 GB of HBM traffic per 1080p frame: 215 B per ray
+// against 127 B at 3 waves (profiles/r04_glass_traffic.json, r04_ab_glass_level_save.txt).
 #ifndef RT_WF_SAVE
-#ifdef RT_LEAN_GENERIC
-#define RT_WF_SAVE 1
-#else
 #define RT_WF_SAVE 0
-#endif
 #endif
 #ifdef RT_LEAN_GENERIC
 #ifndef RT_WF_LEVEL_WAVES
-#define RT_WF_LEVEL_WAVES 4
+#define RT_WF_LEVEL_WAVES 3
 #endif
 constexpr int kWfLevelWaves = RT_WF_LEVEL_WAVES;
 #else
