@@ -74,6 +74,19 @@ constexpr int kFeatNoPL = 32;
 // feature (C2): 6 with its light records read through the scalar cache (80 VGPRs, 48 B/lane of
 // scratch): C2 48.1 -> 46.7 us against 5 waves (95 VGPRs + 20 B, lights from LDS), MI355X
 constexpr int kPkStack = 64;       // wave-coherent BVH walk: node stack entries per wave (depth ≤ 48)
+// A/B options (off): the shading point and normal parked in LDS (6 doubles per lane, structure
+// of arrays) across the area light's sample loop (RT_PK_AREA_PARK) or the point-light loop
+// (RT_PK_PARK_POINT) of the ≤ 64-sphere variants, instead of in registers.  At 80 VGPRs (6
+// waves/SIMD) this cuts C5's spills 116 → 44 B/lane (live scratch 5.6 → 2.2 MB per XCD against a
+// 4 MB L2: HBM traffic 5.25 → 2.44× the framebuffer) and C2's 44 → 12 B/lane (1.47 → 1.15×),
+// but the reloads cost time: C5 414 → 434 µs, C2 38.3 → 38.9 µs per frame
+// (profiles/r04_ab_park.txt, r04_park_traffic.json).
+#ifndef RT_PK_AREA_PARK
+#define RT_PK_AREA_PARK 0
+#endif
+#ifndef RT_PK_PARK_POINT
+#define RT_PK_PARK_POINT 0
+#endif
 #ifndef RT_PACKET_SMALL_WAVES
 #define RT_PACKET_SMALL_WAVES 6
 #endif
@@ -1155,6 +1168,12 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
     if constexpr ((FEAT & kFeatTris) != 0)  // after the image: 64 ints per wave
         S.wstk = reinterpret_cast<int*>(smem + pk_image_bytes(ns, np, nl) / 8) +
                  kPkStack * (tid >> 6);
+    constexpr bool kPark = RT_PK_AREA_PARK && (FEAT & kFeatArea) != 0 && MAXC == 1;
+    constexpr bool kParkPoint = RT_PK_PARK_POINT && MAXC == 1;
+    double* park = nullptr;  // then 6 doubles per lane (stride kThreads)
+    if constexpr (kPark || kParkPoint)
+        park = smem + pk_image_bytes(ns, np, nl) / 8 +
+               ((FEAT & kFeatTris) != 0 ? kPkStack * kThreads / 128 : 0) + tid;
     const int nchunks = (ns + 63) / 64;
 
     const int lane = tid & 63, wave = tid >> 6;
@@ -1250,10 +1269,25 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
                 n = unit(n0);  // directLightning's own normalize (Scene.h:81)
             }
             d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
+            if constexpr (kParkPoint) {
+                park[0 * kThreads] = hp.x;
+                park[1 * kThreads] = hp.y;
+                park[2 * kThreads] = hp.z;
+                park[3 * kThreads] = n.x;
+                park[4 * kThreads] = n.y;
+                park[5 * kThreads] = n.z;
+                __asm__ volatile("" ::: "memory");
+            }
             for (int l = 0; l < nl; ++l) {
                 d3 L, E;
                 pk_light_record<MAXC>(S, P, l, L, E);
-                pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, L, E, L, 0.0, bias, nchunks,
+                d3 hl = hp, nl_ = n;
+                if constexpr (kParkPoint) {
+                    __asm__ volatile("" ::: "memory");
+                    hl = mk(park[0 * kThreads], park[1 * kThreads], park[2 * kThreads]);
+                    nl_ = mk(park[3 * kThreads], park[4 * kThreads], park[5 * kThreads]);
+                }
+                pk_light<MAXC, FEAT, COUNT>(S, hit, hl, nl_, view, h, L, E, L, 0.0, bias, nchunks,
                                             diff, spec, cnt);
             }
             if constexpr ((FEAT & kFeatArea) != 0) {
@@ -1267,6 +1301,15 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
                     // one packet cull for all samples: every sample's casting lanes are hit
                     // lanes with this origin, and every sample point is in (al_c, al_r)
                     const OriginBall B = origin_ball(hit, hp + n * bias);
+                    if constexpr (kPark) {
+                        park[0 * kThreads] = hp.x;
+                        park[1 * kThreads] = hp.y;
+                        park[2 * kThreads] = hp.z;
+                        park[3 * kThreads] = n.x;
+                        park[4 * kThreads] = n.y;
+                        park[5 * kThreads] = n.z;
+                        __asm__ volatile("" ::: "memory");  // no forwarding of the stored values
+                    }
                     const Masks<MAXC> Ma = B.ok ? cull_capsule<MAXC, FEAT>(S, B.c, B.R, al_c, al_r, bias)
                                                 : all_candidates<MAXC>(ns);
                     // When that leaves many candidates (a wide light seen past many spheres),
@@ -1302,7 +1345,13 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !M
                             for (int c = 0; c < MAXC; ++c) Mq.m[c] &= Mc.m[c];
                             Mq.pm &= Mc.pm;
                         }
-                        pk_light<MAXC, FEAT, COUNT>(S, hit, hp, n, view, h, lpos, E, al_c, al_r,
+                        d3 hq = hp, nq = n;
+                        if constexpr (kPark) {
+                            __asm__ volatile("" ::: "memory");  // read back every sample
+                            hq = mk(park[0 * kThreads], park[1 * kThreads], park[2 * kThreads]);
+                            nq = mk(park[3 * kThreads], park[4 * kThreads], park[5 * kThreads]);
+                        }
+                        pk_light<MAXC, FEAT, COUNT>(S, hit, hq, nq, view, h, lpos, E, al_c, al_r,
                                                     bias, nchunks, diff, spec, cnt, &Mq);
                     }
                 }
@@ -1508,6 +1557,9 @@ static void launch_packet_shape(const TraceParams& p, bool count, size_t lds, hi
     // (a launch that records its wave durations for the tile order takes the general variant:
     // the single-sample one carries no recording code)
     if constexpr ((FEAT & kFeatTris) != 0) lds += sizeof(int) * kPkStack * (block.x / 64);
+    if constexpr ((RT_PK_AREA_PARK && (FEAT & kFeatArea) != 0 && MAXC == 1) ||
+                  (RT_PK_PARK_POINT && MAXC == 1))
+        lds += 6 * sizeof(double) * block.x;
     if (count) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, true, true, WGY>), grid, block, lds, stream, p);
     else if (p.aa == 1 && !p.tile_cost) hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, false, WGY>), grid, block, lds, stream, p);
     else hipLaunchKernelGGL((packet_direct_kernel<MAXC, FEAT, false, true, WGY>), grid, block, lds, stream, p);
