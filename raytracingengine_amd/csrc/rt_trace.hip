@@ -124,129 +124,6 @@ __global__ __launch_bounds__(kTileW * kTileH, MINW) void trace_kernel(TraceParam
     }
 }
 
-// Reflection chains with lane refill (RT_CHAIN_REFILL; single-sample frames of scenes with
-// spheres: mirror).  Chains end at very different depths (a ray that escapes the box, a matte
-// sphere, the depth limit), and in trace_kernel a lane whose chain ended idles until the longest
-// chain of its wave is done.  Here a workgroup owns a 32×32-pixel block (16 8×8 tiles) and its
-// lanes take pixels from it through an LDS counter whenever some are idle: one bounce per loop
-// iteration, a lane whose chain ends stores its pixel and the wave refills all its idle lanes at
-// once (one LDS atomic per wave), so lanes stay busy until the block is drained.  Each pixel's
-// chain is trace_chain's (same operations, same order), stored as trace_kernel stores it.
-#ifndef RT_CHAIN_REFILL
-#define RT_CHAIN_REFILL 0
-#endif
-#ifndef RT_CHAIN_REFILL_WAVES
-#define RT_CHAIN_REFILL_WAVES 3
-#endif
-constexpr int kRefillBlock = 32;  // pixels per side of a workgroup's block
-
-template <bool COUNT, bool LDS, int MINW>
-__global__ __launch_bounds__(256, MINW) void chain_refill_kernel(TraceParams P) {
-    extern __shared__ double smem[];
-    __shared__ uint32_t s_next;
-    constexpr uint32_t kBlockPx = kRefillBlock * kRefillBlock;
-    const int tid = threadIdx.x, lane = tid & 63;
-    if (tid == 0) s_next = 0u;
-    SceneView S = stage_scene<LDS>(P, smem, tid, 256);
-    __syncthreads();
-    const uint32_t bx = blockIdx.x * kRefillBlock, by = blockIdx.y * kRefillBlock;
-    const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    Counts cnt{0u, 0u};
-    bool live = false, empty = false;
-    uint32_t x = 0, yl = 0;
-    uint64_t pix = 0;
-    int depth = 0;
-    d3 o = cam, d = mk(0.0, 0.0, 1.0), acc = mk(0.0, 0.0, 0.0);
-    double w = 1.0;
-    for (;;) {
-        const uint64_t idle = __ballot(!live);
-        if (idle && !empty) {  // uniform: refill every idle lane of the wave
-            const int leader = __builtin_ctzll(idle);
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&s_next, static_cast<uint32_t>(__popcll(idle)));
-            base = __shfl(base, leader, 64);
-            empty = base + static_cast<uint32_t>(__popcll(idle)) >= kBlockPx;
-            if (!live) {
-                const uint32_t i = base + __builtin_amdgcn_mbcnt_hi(
-                                              static_cast<uint32_t>(idle >> 32),
-                                              __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(idle), 0u));
-                if (i < kBlockPx) {  // 8×8 tiles, row-major within the block
-                    const uint32_t t = i >> 6, q = i & 63u;
-                    x = bx + (t & 3u) * 8u + (q & 7u);
-                    yl = by + (t >> 2) * 8u + (q >> 3);
-                    if (x < P.width && yl < P.rows) {
-                        const uint32_t y = image_row(P, yl);
-                        pix = static_cast<uint64_t>(y) * P.width + x;
-                        o = cam;
-                        d = camera_dir(P, cam, x, y, pix, 0);
-                        acc = mk(0.0, 0.0, 0.0);
-                        w = 1.0;
-                        depth = 0;
-                        live = true;
-                    }
-                }
-            }
-        }
-        if (!__ballot(live)) {
-            if (empty) break;
-            continue;
-        }
-        if (live) {  // one TraceRay of the chain (trace_chain's loop body)
-            bool fin = false;
-            if (depth >= P.max_rec) {  // TraceRay at depth maxRecursion: the sky (Scene.h:132-134)
-                acc = acc + sky(d) * w;
-                fin = true;
-            } else {
-                const Node nd = shade<false, COUNT>(S, P, o, d, pix, 0u, depth, cnt);
-                acc = acc + nd.value * w;
-                if (!nd.hit || !nd.refl) {
-                    fin = true;
-                } else {
-                    w = w * nd.rw;
-                    o = nd.ro;
-                    d = nd.rd;
-                    ++depth;
-                }
-            }
-            if (fin) {  // GeneratePixelAt with one sample: (0 + colour) / 1
-                const d3 v = sdiv(mk(0.0, 0.0, 0.0) + acc, 1.0);
-                store_pixel(P, static_cast<size_t>(yl) * P.width + x, v);
-                live = false;
-            }
-        }
-    }
-    if constexpr (COUNT) {
-        uint32_t t = cnt.trace, sh = cnt.shadow;
-        for (int off = 32; off > 0; off >>= 1) {
-            t += __shfl_xor(t, off, 64);
-            sh += __shfl_xor(sh, off, 64);
-        }
-        if (lane == 0) {
-            atomicAdd(P.counters + 0, static_cast<unsigned long long>(t));
-            atomicAdd(P.counters + 1, static_cast<unsigned long long>(sh));
-        }
-    }
-}
-
-template <bool COUNT, bool LDS, int MINW>
-static hipError_t launch_refill_one(const TraceParams& p, size_t lds_bytes, hipStream_t stream) {
-    const dim3 grid((p.width + kRefillBlock - 1) / kRefillBlock,
-                    (p.rows + kRefillBlock - 1) / kRefillBlock);
-    hipLaunchKernelGGL((chain_refill_kernel<COUNT, LDS, MINW>), grid, dim3(256),
-                       LDS ? lds_bytes : 0, stream, p);
-    return hipGetLastError();
-}
-
-template <int MINW>
-static hipError_t launch_refill(const TraceParams& p, bool count, bool lds, size_t lds_bytes,
-                                hipStream_t stream) {
-    if (count)
-        return lds ? launch_refill_one<true, true, MINW>(p, lds_bytes, stream)
-                   : launch_refill_one<true, false, MINW>(p, lds_bytes, stream);
-    return lds ? launch_refill_one<false, true, MINW>(p, lds_bytes, stream)
-               : launch_refill_one<false, false, MINW>(p, lds_bytes, stream);
-}
-
 template <int PATH, bool COUNT, bool LDS, int MINW, bool SINGLE, bool NOSPH = false,
           bool SPAR = false>
 static hipError_t launch_one(const TraceParams& p, size_t lds_bytes, hipStream_t stream) {
@@ -287,10 +164,6 @@ static hipError_t launch_path(const TraceParams& p, bool count, bool lds, size_t
         if (sp) return launch_lds<PATH, 3, true, false, true>(p, count, lds, lds_bytes, stream);
         if (p.ns == 0 && p.aa == 1 && !p.redo)
             return launch_lds<PATH, RT_CHAIN_NOSPH_WAVES, true, true>(p, count, lds, lds_bytes, stream);
-#if RT_CHAIN_REFILL
-        if (p.aa == 1 && !p.redo)
-            return launch_refill<RT_CHAIN_REFILL_WAVES>(p, count, lds, lds_bytes, stream);
-#endif
         if (p.aa == 1 && !p.redo) return launch_lds<PATH, 3, true>(p, count, lds, lds_bytes, stream);
         if (p.ns == 0 && !p.redo) return launch_lds<PATH, 3, false, true>(p, count, lds, lds_bytes, stream);
         return launch_lds<PATH, 3, false>(p, count, lds, lds_bytes, stream);
