@@ -238,6 +238,7 @@ def test_gather_batch_rejects_gathered_and_local_output(ctx, comm1):
 
 
 @pytest.mark.parametrize("name,w,h,ranks,block,nf", [("c2", 480, 270, 8, 16, 4),
+                                                     ("c2", 160, 90, 3, 16, 18),  # 16 + 2 launches
                                                      ("c2", 480, 270, 3, 16, 5),
                                                      ("c3", 320, 180, 4, 8, 3),
                                                      ("c2", 200, 40, 4, 16, 2)])
