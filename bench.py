@@ -350,6 +350,7 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     dscene.close()
     return {"elapsed": elapsed, "rays": rays_all, "rays_rank": rays_rank, "ranks": ranks,
             "px": W * H, "rows": rows, "frames": frames, "batch": batch,
+            "gather_bytes_per_frame": max_rows * W * 3 if split else 0,
             "bufs": (local, ldr)}
 
 
@@ -357,13 +358,22 @@ def per_rank_summary(res):
     ranks = res["ranks"]
     render = [r[0] for r in ranks]
     mean = sum(render) / len(render)
-    return {
+    gb = res.get("gather_bytes_per_frame", 0)
+    out = {
         "per_rank": [{"rank": i, "rows": int(r[3]), "rays_per_frame": int(r[4]),
                       "render_ms_per_frame": round(r[0], 6), "gather_ms_per_frame": round(r[1], 6),
                       "assemble_ms_per_frame": round(r[2], 6), "timed_frames": int(r[5])}
                      for i, r in enumerate(ranks)],
         "render_imbalance": round(max(render) / mean, 4) if mean > 0 else None,
     }
+    if gb and len(ranks) > 1:
+        # bytes each rank sends per frame (its padded rows of Reinhard bytes) and the rate its
+        # gather reached, from the end of its render to the end of the gather (the link rate
+        # the row split depends on: DESIGN §6)
+        out["gather_bytes_per_rank_frame"] = gb
+        out["gather_GBps_per_rank"] = [round(gb / (r[1] * 1e-3) / 1e9, 2) if r[1] > 0 else None
+                                       for r in ranks]
+    return out
 
 
 def single_launch_frames(R: Runner, sc, frames, warmup, tonemap=1):
