@@ -61,6 +61,10 @@ def parse_args(argv=None):
                     help="rows per block of the block-cyclic split (N>1)")
     ap.add_argument("--hdr", choices=["f64", "f32"], default="f64",
                     help="the rank-local HDR framebuffer: f64 = the reference's std::vector<Vec3>")
+    ap.add_argument("--root-weight", default="auto",
+                    help="N>1: rank 0's share of the row split (rt_comm_set_root_weight): an "
+                         "integer, or 'auto' = chosen from an untimed equal-split probe of the "
+                         "ranks' render and gather times (1 unless the gathers are link-bound)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="gather on the render stream (no overlap of batch b's gather with "
                          "batch b+1's render)")
@@ -281,28 +285,68 @@ class Runner:
 
 
 # ------------------------------------------------------------------------------ the headline
+def choose_root_weight(n, render_ms, gather_ms, max_weight=16, margin=0.9):
+    """Weight of rank 0's share (rt_comm_set_root_weight) from an equal-split probe: render_ms
+    per rank and frame (≈ T/n each, T the whole frame on one GPU) and the ranks' gather times
+    per frame (a peer's 1/n of the frame over its link: ≈ L/n, L the whole frame's bytes over one
+    link, when the gather is link-bound).  With weight w the frame is dealt over V = w + n − 1
+    row sets: rank 0 renders w/V of it (its rows never cross a link), a peer renders 1/V and
+    sends 1/V.  Predicted frame time max(T·w/V, max(T, L)/V); w > 1 only when it beats the
+    equal split's max(T/n, L/n) by the margin."""
+    if n <= 1 or not render_ms or min(render_ms) <= 0:
+        return 1
+    T = sum(render_ms)
+    L = max(gather_ms) * n if gather_ms else 0.0
+    equal = max(T / n, L / n)
+    best_w, best_t = 1, equal
+    for w in range(2, max_weight + 1):
+        V = w + n - 1
+        t = max(T * w / V, max(T, L) / V)
+        if t < best_t:
+            best_w, best_t = w, t
+    return best_w if best_t < margin * equal else 1
+
+
 def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, block=16,
-                 pipeline=True, event_every=4, camera_step=None, gather=True):
+                 pipeline=True, event_every=4, camera_step=None, gather=True, weight=1):
     """Frames of `sc` split over the ranks (block-cyclic rows), `batch` frames per
     rt_render_gather_batch call: this rank's rows of the HDR framebuffer stay on the rank, the
-    fused bytes are gathered to rank 0 (one ncclGather per batch; none at N=1) and assembled.
+    fused bytes are gathered to rank 0 (one gather per batch; none at N=1) and assembled.
     gather=False: every rank renders whole frames of its own (weak scaling; same call on a
-    one-rank view).  camera_step(base, frame) -> a new camera position per frame."""
+    one-rank view).  camera_step(base, frame) -> a new camera position per frame.
+    weight > 1: rank 0 renders `weight` of the weight + N − 1 row sets (rt_comm_set_root_weight)."""
     torch, capi = R.torch, R.capi
     W, H = sc.camera.width, sc.camera.height
     dscene = R.ctx.scene(sc)
     split = gather and R.world > 1
-    plan = R.rank_plan(H, block) if split else capi.default_opts(tonemap=-1)
-    rows = capi.rendered_rows(plan, H) if plan.row_begin < H else 0
-    # rt_render_gather_batch lays every rank's frames max_rows rows apart (the largest rank's)
-    max_rows = max(capi.rendered_rows(R.rank_plan(H, block, r), H) for r in range(R.world)
-                   if r * block < H) if split else rows
-    rays_rank = R.count_rays(dscene, plan) if rows else 0
+    weight = weight if split else 1
+    V = weight + R.world - 1 if split else 1
+    # this rank's row sets ("slots") of the V-slot split: rank 0 slots [0, weight), rank r ≥ 1
+    # slot weight + r − 1
+    def slot_plan(s):
+        o = capi.default_opts(tonemap=-1)
+        o.row_begin, o.row_end, o.row_block, o.row_cycle = s * block, H, block, V
+        return o
+    if split:
+        my_slots = list(range(weight)) if R.rank == 0 else [weight + R.rank - 1]
+        slot_plans = [slot_plan(s) for s in my_slots]
+        plan = slot_plans[0]
+    else:
+        slot_plans = [capi.default_opts(tonemap=-1)]
+        plan = slot_plans[0]
+    slot_rows = [capi.rendered_rows(p, H) if p.row_begin < H else 0 for p in slot_plans]
+    rows = sum(slot_rows)
+    # rt_render_gather_batch lays every row set's frames max_rows rows apart (the largest set's)
+    max_rows = max(capi.rendered_rows(slot_plan(s), H) for s in range(V)
+                   if s * block < H) if split else rows
+    rays_rank = sum(R.count_rays(dscene, p) for p, r in zip(slot_plans, slot_rows) if r)
     comm = R.comm if split else R.solo_comm()
+    if split:
+        comm.set_root_weight(weight)
     # two sets of buffers (the pipelined slots): batch b writes set b mod 2
     hdr_dtype = torch.float64 if hdr == "f64" else torch.float32
-    local = [torch.empty(max(max_rows, 1) * W * 3 * batch, dtype=hdr_dtype, device="cuda")
-             for _ in range(2)]
+    local = [torch.empty(max(max_rows, 1) * W * 3 * batch * len(slot_plans), dtype=hdr_dtype,
+                         device="cuda") for _ in range(2)]
     root = R.rank == 0 or not split
     ldr = [torch.empty(H * W * 3 * batch if root else 1, dtype=torch.uint8, device="cuda")
            for _ in range(2)]
@@ -343,6 +387,8 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     comm.timing(reset=True)
     elapsed, _ = R.timed(step, frames, warmup, batch, warm_step=warm_step if split else None)
     t = comm.timing(reset=True)
+    if split and weight != 1:
+        comm.set_root_weight(1)
     per_frame = [t.render_ms / max(t.frames, 1), t.gather_ms / max(t.frames, 1),
                  t.assemble_ms / max(t.frames, 1), float(rows), float(rays_rank), float(t.frames)]
     ranks = R.gather_rows(per_frame)
@@ -350,7 +396,7 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     dscene.close()
     return {"elapsed": elapsed, "rays": rays_all, "rays_rank": rays_rank, "ranks": ranks,
             "px": W * H, "rows": rows, "frames": frames, "batch": batch,
-            "gather_bytes_per_frame": max_rows * W * 3 if split else 0,
+            "gather_bytes_per_frame": max_rows * W * 3 if split else 0, "root_weight": weight,
             "bufs": (local, ldr)}
 
 
@@ -449,8 +495,22 @@ def main(argv=None):
     extras = not args.no_extras
     batch = max(1, args.batch)
 
+    weight, probe = 1, None
+    if R.world > 1 and args.root_weight != "1":
+        if args.root_weight == "auto":
+            # untimed equal-split probe: every batch timed with events
+            pr = split_frames(R, sc, 8 * batch, batch, batch, args.hdr, tonemap, args.row_block,
+                              not args.no_pipeline, 1)
+            render = [r[0] for r in pr["ranks"]]
+            gath = [r[1] for r in pr["ranks"]]
+            (w,) = R.max_over_ranks(float(choose_root_weight(R.world, render, gath)))
+            weight = int(w)
+            probe = {"render_ms_per_frame": [round(x, 6) for x in render],
+                     "gather_ms_per_frame": [round(x, 6) for x in gath], "chosen": weight}
+        else:
+            weight = max(1, int(args.root_weight))
     res = split_frames(R, sc, args.steps, args.warmup, batch, args.hdr, tonemap, args.row_block,
-                       not args.no_pipeline, args.event_every)
+                       not args.no_pipeline, args.event_every, weight=weight)
     elapsed = res["elapsed"]
     value = res["rays"] * args.steps / elapsed / 1e6
     summ = per_rank_summary(res)
@@ -476,11 +536,16 @@ def main(argv=None):
             "workload": workload_text(sc, R.world, args.row_block, batch, args.hdr,
                                       args.tonemap),
             "global_batch": args.steps, "resolution": [W, H],
-            "parallelism": f"block-cyclic rows ({args.row_block}-row blocks) x{R.world} + one "
-                           f"ncclGather per batch of frames",
+            "parallelism": (f"block-cyclic rows ({args.row_block}-row blocks) x{R.world} + one "
+                            f"ncclGather per batch of frames" if weight == 1 else
+                            f"block-cyclic rows ({args.row_block}-row blocks) in {weight + R.world - 1} "
+                            f"row sets, {weight} on rank 0 + one on each other rank, one group of "
+                            f"P2P sends to rank 0 per batch of frames"),
+            "root_weight": weight,
             "frames_per_call": batch, "rays_per_frame": int(res["rays"]),
         },
         "frames_per_sec": round(args.steps / elapsed, 3),
+        "root_weight_probe": probe,
         "clock_warmup_ms": args.clock_warmup_ms,
         "kernel_ms_per_frame": round(render_ms, 6),
         "kernel_ms_per_launch": round(render_ms * batch, 6),

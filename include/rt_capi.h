@@ -266,6 +266,14 @@ rt_status rt_comm_create_all(rt_context* const* ctxs, int n, rt_comm** comms_out
 rt_status rt_comm_create_local(rt_context* const* ctxs, int n, rt_comm** comms_out);
 rt_status rt_comm_destroy(rt_comm* comm);
 rt_status rt_comm_info(const rt_comm* comm, int* nranks, int* rank);
+/* Weighted row split (every rank of the communicator sets the same weight before its next frame;
+ * default 1): the frame's blocks are dealt over weight + n − 1 row sets, rank 0 renders `weight`
+ * of them and every other rank one — rank 0's rows never cross a link, so when the peers' gathers
+ * are link-bound it takes a larger share.  With weight > 1 the gather is a group of P2P sends of
+ * equal counts (ncclSend / ncclRecv) into rank 0's receive buffer, where rank 0 renders its own
+ * row sets in place; rank-local outputs of rank 0 hold its row sets one after another (each
+ * nframes*max_rows*W*3 elements).  rt_gather_timing.rows is a rank's total. */
+rt_status rt_comm_set_root_weight(rt_comm* comm, int weight);
 /* Collective: every rank calls it with the same camera, opts and outputs (RT_OUT_* bits).  The
  * scene belongs to the communicator's context.  On rank 0 the d_* are whole-frame device
  * framebuffers (W*H*3 elements, image order) for every requested output; elsewhere ignored.

@@ -41,7 +41,7 @@ EXPORTED = [
     "rt_context_destroy", "rt_context_set_stream", "rt_context_synchronize", "rt_scene_create",
     "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
     "rt_render_multi", "rt_comm_unique_id", "rt_comm_create", "rt_comm_create_all",
-    "rt_comm_create_local", "rt_comm_destroy", "rt_comm_info", "rt_render_gather", "rt_render_gather_all",
+    "rt_comm_create_local", "rt_comm_destroy", "rt_comm_info", "rt_comm_set_root_weight", "rt_render_gather", "rt_render_gather_all",
     "rt_comm_timing", "rt_comm_synchronize", "rt_debug_assemble_rows", "rt_debug_tile_order",
     "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
     "rt_debug_f64_ops", "rt_debug_vec_ops", "rt_queue_create", "rt_queue_destroy",
@@ -138,6 +138,7 @@ def load_library(path: str = LIB_PATH):
         "rt_comm_create_local": [vp, i32, vp],
         "rt_comm_destroy": [vp],
         "rt_comm_info": [vp, vp, vp],
+        "rt_comm_set_root_weight": [vp, i32],
         "rt_render_gather": [vp, vp, vp, vp, i32, vp, vp, vp],
         "rt_render_gather_all": [vp, vp, i32, vp, vp, i32, vp, vp, vp],
         "rt_render_gather_batch": [vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp],
@@ -531,6 +532,11 @@ class Comm:
 
     def synchronize(self):
         _check(_lib.rt_comm_synchronize(self._h))
+
+    def set_root_weight(self, weight: int):
+        """Weighted row split (rt_comm_set_root_weight): rank 0 renders `weight` of the
+        weight + n − 1 row sets, every other rank one; the same value on every rank."""
+        _check(_lib.rt_comm_set_root_weight(self._h, int(weight)))
 
     def timing(self, reset: bool = False) -> GatherTiming:
         t = GatherTiming()

@@ -39,6 +39,9 @@ struct rt_comm {
     std::vector<rt_comm*> peers;
     hipEvent_t xfer_ready = nullptr, xfer_done = nullptr;
     int nranks = 1, rank = 0;
+    // rt_comm_set_root_weight: rank 0 renders `root_weight` row sets (slots) of the block-cyclic
+    // split, every other rank one; > 1 gathers with grouped P2P sends instead of ncclGather
+    int root_weight = 1;
     // Two frame slots (RT_FLAG_PIPELINE alternates them; otherwise slot 0).  Per slot and output
     // kind (RT_OUT_HDR64, _HDR32, _LDR): this rank's packed rows (send) and, on rank 0, the n
     // gathered buffers (recv).
@@ -84,11 +87,24 @@ rt_status nccl_fail(ncclResult_t r, const char* what) {
 // This rank's share of the frame: rt_render_opts selecting the block-cyclic row set `rank` of
 // `n` (a contiguous full frame when n == 1), and the rows it produces.
 struct Plan {
-    rt_render_opts opts;
+    rt_render_opts opts;  // the first slot's
     uint32_t block = 0, rows = 0, max_rows = 0;
+    // the split's row sets ("slots"): V = root_weight + n − 1 of them, dealt block-cyclically;
+    // rank 0 owns slots [0, root_weight), rank r ≥ 1 slot root_weight + r − 1
+    int slots = 1, first_slot = 0, nslots = 1;
+    uint32_t slot_rows[64];  // rows of each of this rank's slots
 };
 
-rt_status make_plan(const rt_camera* cam, const rt_render_opts* in, int n, int rank, Plan& pl) {
+// Slot s of a V-slot block-cyclic split of H rows in blocks of b: opts and rows.
+void slot_opts(const rt_render_opts& base, uint32_t b, int V, int s, rt_render_opts& o) {
+    o = base;
+    o.row_begin = static_cast<uint32_t>(s) * b;
+    o.row_block = static_cast<uint16_t>(b);
+    o.row_cycle = static_cast<uint16_t>(V);
+}
+
+rt_status make_plan(const rt_camera* cam, const rt_render_opts* in, int n, int rank, Plan& pl,
+                    int weight = 1) {
     rt_render_opts o;
     if (in) o = *in;
     else rt_render_opts_default(&o);
@@ -104,9 +120,28 @@ rt_status make_plan(const rt_camera* cam, const rt_render_opts* in, int n, int r
     pl.opts = o;
     pl.rows = o.row_begin < H ? rendered_rows(o, H) : 0;
     pl.max_rows = 0;
-    for (int r = 0; r < n; ++r) {
-        rt_render_opts q = o;
-        q.row_begin = static_cast<uint32_t>(r) * pl.block;
+    pl.slots = n;
+    pl.first_slot = rank;
+    pl.nslots = 1;
+    pl.slot_rows[0] = pl.rows;
+    if (n > 1 && weight > 1) {  // the weighted split: V slots, rank 0 owns `weight` of them
+        const int V = weight + n - 1;
+        pl.slots = V;
+        pl.first_slot = rank == 0 ? 0 : weight + rank - 1;
+        pl.nslots = rank == 0 ? weight : 1;
+        pl.rows = 0;
+        for (int j = 0; j < pl.nslots; ++j) {
+            rt_render_opts q;
+            slot_opts(o, pl.block, V, pl.first_slot + j, q);
+            pl.slot_rows[j] = q.row_begin < H ? rendered_rows(q, H) : 0;
+            pl.rows += pl.slot_rows[j];
+        }
+        slot_opts(o, pl.block, V, pl.first_slot, pl.opts);
+    }
+    for (int r = 0; r < pl.slots; ++r) {
+        rt_render_opts q;
+        slot_opts(o, pl.block, pl.slots, r, q);
+        if (n == 1) q = o;
         if (q.row_begin < H) pl.max_rows = std::max(pl.max_rows, rendered_rows(q, H));
     }
     return RT_OK;
@@ -174,9 +209,10 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cams, int
     if (sc->ctx != ctx)
         return fail(RT_ERR_INVALID_ARG, "scene does not belong to the communicator's context");
     const rt_camera* cam = cams;
-    rt_status st = make_plan(cam, opts, c->nranks, c->rank, f.pl);
+    rt_status st = make_plan(cam, opts, c->nranks, c->rank, f.pl, c->root_weight);
     if (st != RT_OK) return st;
     Plan& pl = f.pl;
+    const bool weighted = pl.slots > c->nranks;  // rank 0's slots land in its receive buffer
     f.nframes = nframes;
     // one rank: its rows are the whole frame in image order, rendered straight into the
     // caller's framebuffers (no send buffer, no gather, no assembly)
@@ -187,8 +223,10 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cams, int
     const size_t npx = static_cast<size_t>(pl.max_rows) * cam->width * nframes;
     for (int k = 0; k < 3 && !f.direct; ++k) {
         if (!(outputs & kOutputs[k])) continue;
-        RT_HIP(c->send[f.slot][k].ensure(send_bytes(pl, cam->width, nframes, k)));
-        if (c->rank == 0) RT_HIP(c->recv[f.slot][k].ensure(npx * bytes_per_px(k) * c->nranks));
+        if (!(weighted && c->rank == 0))
+            RT_HIP(c->send[f.slot][k].ensure(send_bytes(pl, cam->width, nframes, k)));
+        if (c->rank == 0)
+            RT_HIP(c->recv[f.slot][k].ensure(npx * bytes_per_px(k) * static_cast<size_t>(pl.slots)));
     }
     c->rows = pl.rows;
     c->max_rows = pl.max_rows;
@@ -222,12 +260,32 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cams, int
             RT_HIP(hipStreamWaitEvent(ctx->stream, c->freed[s], 0));
     st = record(f.ev, 0, ctx->stream);
     if (st != RT_OK) return st;
-    if (pl.rows > 0) {
+    // each of this rank's slots: all frames in one launch, frames max_rows rows apart; a slot's
+    // outputs follow the previous slot's (rank-local outputs), or — rank 0 of a weighted split —
+    // sit at the slot's place in the receive buffer, where the assembly reads them
+    const size_t slot_px = static_cast<size_t>(nframes) * pl.max_rows * cam->width;
+    for (int j = 0; j < pl.nslots; ++j) {
+        if (pl.slot_rows[j] == 0) continue;
+        rt_render_opts so = pl.opts;
+        if (weighted) slot_opts(pl.opts, pl.block, pl.slots, pl.first_slot + j, so);
         void* out[3];
-        for (int k = 0; k < 3; ++k)
-            out[k] = !(outputs & kOutputs[k]) ? (local ? local[k] : nullptr)
-                                              : (f.direct ? dst[k] : c->send[f.slot][k].ptr);
-        st = enqueue_frames(ctx, sc, cams, nframes, &pl.opts, static_cast<double*>(out[0]),
+        for (int k = 0; k < 3; ++k) {
+            const size_t off = j * slot_px * 3;  // elements
+            char* base;
+            if (!(outputs & kOutputs[k])) {
+                base = local && local[k] ? static_cast<char*>(local[k]) + off * (k == 0 ? 8 : k == 1 ? 4 : 1)
+                                         : nullptr;
+            } else if (f.direct) {
+                base = static_cast<char*>(dst[k]);
+            } else if (weighted && c->rank == 0) {
+                base = static_cast<char*>(c->recv[f.slot][k].ptr) +
+                       static_cast<size_t>(pl.first_slot + j) * slot_px * bytes_per_px(k);
+            } else {
+                base = static_cast<char*>(c->send[f.slot][k].ptr);
+            }
+            out[k] = base;
+        }
+        st = enqueue_frames(ctx, sc, cams, nframes, &so, static_cast<double*>(out[0]),
                             static_cast<float*>(out[1]), static_cast<uint8_t*>(out[2]),
                             pl.max_rows);
         if (st != RT_OK) return st;
@@ -245,6 +303,24 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cams, int
 // buffer's nframes·max_rows rows land in slot `rank` of rank 0's receive buffer.
 rt_status gather_part(rt_comm* c, const rt_camera* cam, int outputs, const Frame& f) {
     if (f.direct) return RT_OK;
+    if (f.pl.slots > c->nranks) {
+        // weighted split: rank 0's own slots are already in place; each other rank's one slot
+        // goes to its place in rank 0's receive buffer (grouped P2P, equal counts)
+        const int w = f.pl.slots - c->nranks + 1;
+        for (int k = 0; k < 3; ++k) {
+            if (!(outputs & kOutputs[k])) continue;
+            const size_t count = send_bytes(f.pl, cam->width, f.nframes, k);
+            if (c->rank == 0) {
+                char* recv = static_cast<char*>(c->recv[f.slot][k].ptr);
+                for (int r = 1; r < c->nranks; ++r)
+                    RT_NCCL(ncclRecv(recv + static_cast<size_t>(w + r - 1) * count, count,
+                                     ncclUint8, r, c->nccl, f.gs));
+            } else {
+                RT_NCCL(ncclSend(c->send[f.slot][k].ptr, count, ncclUint8, 0, c->nccl, f.gs));
+            }
+        }
+        return RT_OK;
+    }
     for (int k = 0; k < 3; ++k) {
         if (!(outputs & kOutputs[k])) continue;
         char* send = static_cast<char*>(c->send[f.slot][k].ptr);
@@ -278,14 +354,16 @@ rt_status gather_local(rt_comm* const* comms, int n, const rt_camera* cam, int o
         if (!(outputs & kOutputs[k])) continue;
         const size_t bytes = send_bytes(f0.pl, cam->width, f0.nframes, k);
         char* recv = static_cast<char*>(root->recv[f0.slot][k].ptr);
-        for (int i = 0; i < n; ++i) {  // rank i's whole batch into slot i, as ncclGather does
+        // weighted split: rank 0's slots are in place, rank i's slot is w + i − 1
+        const int w = f0.pl.slots - n + 1;
+        for (int i = (w > 1 ? 1 : 0); i < n; ++i) {  // rank i's whole batch into its slot
             const void* send = comms[i]->send[f[i].slot][k].ptr;
+            const size_t at = static_cast<size_t>(w > 1 ? w + i - 1 : i) * bytes;
             if (comms[i]->device == root->device)
-                RT_HIP(hipMemcpyAsync(recv + i * bytes, send, bytes, hipMemcpyDeviceToDevice,
-                                      f0.gs));
+                RT_HIP(hipMemcpyAsync(recv + at, send, bytes, hipMemcpyDeviceToDevice, f0.gs));
             else
-                RT_HIP(hipMemcpyPeerAsync(recv + i * bytes, root->device, send, comms[i]->device,
-                                          bytes, f0.gs));
+                RT_HIP(hipMemcpyPeerAsync(recv + at, root->device, send, comms[i]->device, bytes,
+                                          f0.gs));
         }
     }
     RT_HIP(hipEventRecord(root->xfer_done, f0.gs));
@@ -307,7 +385,7 @@ rt_status assemble_part(rt_comm* c, const rt_camera* cam, int outputs, const Fra
             if (!(outputs & kOutputs[k]) || !dst[k]) continue;
             RT_HIP(launch_assemble_rows(c->recv[f.slot][k].ptr, dst[k],
                                         size_t(cam->width) * bytes_per_px(k), cam->height,
-                                        f.pl.block, static_cast<uint32_t>(c->nranks),
+                                        f.pl.block, static_cast<uint32_t>(f.pl.slots),
                                         f.pl.max_rows, static_cast<uint32_t>(f.nframes), f.gs));
         }
     }
@@ -865,6 +943,22 @@ rt_status rt_debug_assemble_rows(rt_context* ctx, const void* gathered, size_t r
                                 ctx->stream));
     RT_HIP(hipMemcpyAsync(image, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     RT_HIP(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+rt_status rt_comm_set_root_weight(rt_comm* c, int weight) {
+    if (!c) return fail(RT_ERR_INVALID_ARG, "comm is NULL");
+    if (weight < 1 || weight > 64)
+        return fail(RT_ERR_INVALID_ARG, "root weight must be in [1, 64]");
+    if (weight > 1 && c->nranks + weight - 1 > 65535)
+        return fail(RT_ERR_INVALID_ARG, "too many row sets");
+    if (c->any_frame && weight != c->root_weight) {
+        // frames in flight were planned with the old weight: wait for them
+        DeviceGuard g(c->device);
+        RT_HIP(hipStreamSynchronize(c->ctx->stream));
+        RT_HIP(hipStreamSynchronize(c->gstream));
+    }
+    c->root_weight = weight;
     return RT_OK;
 }
 

@@ -279,3 +279,51 @@ def test_gather_all_batch_local_ranks_is_the_frames(name, w, h, ranks, block, nf
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize("name,w,h,ranks,block,nf,weight", [
+    ("c2", 480, 270, 8, 16, 4, 3), ("c2", 480, 270, 2, 16, 3, 2), ("c3", 320, 180, 4, 8, 3, 4),
+    ("c2", 200, 40, 4, 16, 2, 2),   # some row sets empty
+    ("c2", 160, 90, 3, 16, 18, 2),  # 16 + 2 frames per row set
+    ("glass", 160, 120, 3, 16, 2, 2)])
+def test_gather_all_batch_weighted_root_is_the_frames(name, w, h, ranks, block, nf, weight):
+    """The weighted split (rt_comm_set_root_weight): the blocks dealt over weight + n − 1 row
+    sets, rank 0 renders `weight` of them straight into its receive buffer, every other rank
+    one, moved into place by the gather (device copies here; P2P sends on RCCL communicators),
+    then the same assembly.  Every frame = the single-rank frame, pipelined or not, and the
+    communicators switch back to weight 1 between frames."""
+    ctxs = [capi.Context(0) for _ in range(ranks)]
+    try:
+        comms = capi.Comm.create_local(ctxs)
+        sc = make_config(name, w, h)
+        scenes = [c.scene(sc) for c in ctxs]
+        pos = _positions(scenes[0], nf, seed=17)
+        refs = [_single(scenes[0], p, capi.default_opts(tonemap=1), h, w) for p in pos]
+        for wt, pipeline in ((weight, False), (weight, True), (1, True)):
+            for c in comms:
+                c.set_root_weight(wt)
+            opts = capi.default_opts(tonemap=1, row_block=block,
+                                     flags=capi.RT_FLAG_PIPELINE if pipeline else 0)
+            L8 = torch.zeros(nf * h * w * 3, dtype=torch.uint8, device="cuda")
+            H64 = torch.zeros(nf * h * w * 3, dtype=torch.float64, device="cuda")
+            torch.cuda.synchronize()
+            capi.render_gather_all_batch(comms, scenes, scenes[0].cameras(pos), opts,
+                                         capi.RT_OUT_LDR | capi.RT_OUT_HDR64,
+                                         d_hdr64=H64.data_ptr(), d_ldr=L8.data_ptr())
+            for c in comms:
+                c.synchronize()
+            a8 = L8.cpu().numpy().reshape(nf, -1)
+            a64 = H64.cpu().numpy().reshape(nf, -1)
+            for f in range(nf):
+                assert np.array_equal(a8[f], refs[f][1]), (wt, pipeline, f)
+                assert np.array_equal(a64[f], refs[f][0]), (wt, pipeline, f)
+        with pytest.raises(capi.RtError) as e:
+            comms[0].set_root_weight(0)
+        assert e.value.status == capi.RT_ERR_INVALID_ARG
+        for s in scenes:
+            s.close()
+        for c in comms:
+            c.close()
+    finally:
+        for c in ctxs:
+            c.close()
