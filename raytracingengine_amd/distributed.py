@@ -48,6 +48,61 @@ def plan_rows(ranges: list[tuple[int, int]]) -> int:
     return sum(b - a for a, b in ranges)
 
 
+def weighted_slots(rank: int, world: int, weight: int) -> list[int]:
+    """Row sets ("slots") of `rank` in the weighted split (rt_comm_set_root_weight): the blocks
+    are dealt over weight + world − 1 sets, rank 0 owns sets [0, weight), rank r ≥ 1 set
+    weight + r − 1."""
+    if weight < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank/world/weight")
+    return list(range(weight)) if rank == 0 else [weight + rank - 1]
+
+
+def gather_frames_weighted(slots: list[torch.Tensor], nframes: int, height: int, width: int,
+                           weight: int, channels: int = 3, group=None,
+                           block: int = DEFAULT_BLOCK) -> torch.Tensor | None:
+    """The weighted split of rt_render_gather_batch with weight > 1 (rt_multi.cpp): `slots`
+    holds this rank's row sets (weighted_slots), each [nframes * rows_of_set, width, channels]
+    with the frames back to back.  Rank 0's own sets stay in place; every other rank sends its
+    one set, padded to max_rows rows per frame, with a point-to-point send (one group of equal
+    counts, as ncclSend / ncclRecv), and rank 0 writes every set's rows into image order —
+    [nframes, height, width, channels] there, None elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    V = weight + world - 1
+    sets = [row_ranges(s, V, height, block) for s in range(V)]
+    max_rows = max(plan_rows(p) for p in sets)
+    mine = weighted_slots(rank, world, weight)
+    if len(slots) != len(mine):
+        raise ValueError(f"rank {rank}: {len(slots)} row sets, expected {len(mine)}")
+
+    def padded(t, s):
+        rows = plan_rows(sets[s])
+        if t.shape[0] != nframes * rows:
+            raise ValueError(f"set {s}: {t.shape[0]} rows, expected {nframes} x {rows}")
+        out = torch.zeros((nframes, max_rows, width, channels), dtype=t.dtype)
+        out[:, :rows] = t.reshape(nframes, rows, width, channels)
+        return out
+
+    if rank != 0:
+        dist.send(padded(slots[0], mine[0]).contiguous(), dst=0, group=group)
+        return None
+    recv = [None] * V
+    for j, s in enumerate(mine):
+        recv[s] = padded(slots[j], s)
+    for r in range(1, world):
+        buf = torch.empty((nframes, max_rows, width, channels), dtype=slots[0].dtype)
+        dist.recv(buf, src=r, group=group)
+        recv[weight + r - 1] = buf
+    frames = torch.empty((nframes, height, width, channels), dtype=slots[0].dtype)
+    for f in range(nframes):
+        for s in range(V):
+            k = 0
+            for a, b in sets[s]:
+                frames[f, a:b] = recv[s][f, k: k + (b - a)]
+                k += b - a
+    return frames
+
+
 def gather_rows(tile: torch.Tensor, height: int, width: int, channels: int = 3,
                 group=None, block: int = 0) -> torch.Tensor | None:
     """Gather every rank's [rows, width, channels] tile to rank 0 and return the full
