@@ -289,14 +289,16 @@ def choose_root_weight(n, render_ms, gather_ms, max_weight=16, margin=0.9):
     """Weight of rank 0's share (rt_comm_set_root_weight) from an equal-split probe: render_ms
     per rank and frame (≈ T/n each, T the whole frame on one GPU) and the ranks' gather times
     per frame (a peer's 1/n of the frame over its link: ≈ L/n, L the whole frame's bytes over one
-    link, when the gather is link-bound).  With weight w the frame is dealt over V = w + n − 1
+    link, when the gather is link-bound; the fastest peer's, since a gather also waits for the
+    other side to be ready).  With weight w the frame is dealt over V = w + n − 1
     row sets: rank 0 renders w/V of it (its rows never cross a link), a peer renders 1/V and
     sends 1/V.  Predicted frame time max(T·w/V, max(T, L)/V); w > 1 only when it beats the
     equal split's max(T/n, L/n) by the margin."""
     if n <= 1 or not render_ms or min(render_ms) <= 0:
         return 1
     T = sum(render_ms)
-    L = max(gather_ms) * n if gather_ms else 0.0
+    peers = [g for g in gather_ms[1:] if g > 0] if gather_ms else []
+    L = min(peers) * n if peers else 0.0
     equal = max(T / n, L / n)
     best_w, best_t = 1, equal
     for w in range(2, max_weight + 1):

@@ -24,6 +24,13 @@ def test_link_bound_peers_shift_rows_to_rank0():
     assert choose_root_weight(8, [0.0048] * 8, [0.0128] * 8) >= 2
 
 
+def test_link_estimate_is_the_fastest_peer():
+    # rank 0's gather waits for the slowest peer and one peer waited for rank 0: the fastest
+    # peer's gather is the link time
+    assert choose_root_weight(4, [0.0096] * 4, [0.05, 0.0101, 0.03, 0.0099]) == 1
+    assert choose_root_weight(2, [0.0193] * 2, [0.2, 0.051]) == 3
+
+
 def test_degenerate_probes():
     assert choose_root_weight(4, [], []) == 1
     assert choose_root_weight(4, [0.0, 0.01, 0.01, 0.01], [0.05] * 4) == 1
