@@ -11,7 +11,7 @@ Contract (driver):  python bench.py --gpus N --steps K --warmup W
     bytes into its send buffer), ONE ncclGather per batch moves the bytes to rank 0 over xGMI,
     and rank 0 writes them into image order (rt_render_gather_batch).  At N=1 the one rank's
     rows are the frame: it renders straight into the frame buffers, nothing to gather.
-  * Frames go in batches of --batch (default 16) per call: one render launch per batch (one
+  * Frames go in batches of --batch (default 32) per call: one render launch per batch (one
     grid plane per frame, so a small per-rank share of a frame does not pay a whole launch's
     ramp and drain), one ncclGather and one assembly launch per batch; two
     batches in flight (RT_FLAG_PIPELINE: batch b's gather overlaps batch b+1's render).
@@ -53,8 +53,8 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=20, help="untimed frames after the clock warm-up")
     ap.add_argument("--config", default="c2",
                     help="c1..c5 (BASELINE configs), mirror, glass, mesh, bigmesh; default c2")
-    ap.add_argument("--batch", type=int, default=16,
-                    help="frames per rt_render_gather_batch call (1..16 per launch)")
+    ap.add_argument("--batch", type=int, default=32,
+                    help="frames per rt_render_gather_batch call (up to 32 per launch)")
     ap.add_argument("--tonemap", default="reinhard_simple",
                     help="fused LDR operator (the gathered bytes)")
     ap.add_argument("--row-block", type=int, default=16,
@@ -358,7 +358,7 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
                               flags=pf | capi.RT_FLAG_TIME_KERNEL)
     base = dscene.camera["position"][0].copy()
     static_cams = dscene.cameras([base] * batch)
-    nb = [0]
+    nb, nt = [0], [0]
 
     def cams_for(f0, n):
         if camera_step is None:
@@ -368,7 +368,10 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     def step(f0, n, timed):
         b = nb[0]
         nb[0] += 1
-        ev = timed and event_every > 0 and b % event_every == 0
+        # HIP events around every event_every-th TIMED batch, the first one included
+        ev = timed and event_every > 0 and nt[0] % event_every == 0
+        if timed:
+            nt[0] += 1
         kw = {"rank_hdr64": local[b & 1].data_ptr()} if hdr == "f64" else \
              {"rank_hdr32": local[b & 1].data_ptr()}
         comm.render_gather_batch(dscene, cams_for(f0, n), topts if ev else opts, capi.RT_OUT_LDR,

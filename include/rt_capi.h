@@ -320,7 +320,7 @@ rt_status rt_render_device(rt_context* ctx, const rt_scene* scene, const rt_came
  * — views of one scene from several positions (an animation's frames, a camera path) — into
  * device buffers holding the frames back to back (frame f at f*rows*W*3 elements of each
  * output).  Every camera must have cams[0]'s width, height, focal and aa_samples; the position
- * may differ.  Scenes the packet kernel renders (no secondary rays) take up to 16 frames per
+ * may differ.  Scenes the packet kernel renders (no secondary rays) take up to 32 frames per
  * launch (one grid plane per frame), so the launch's ramp and drain are paid once per batch;
  * other scenes take one launch per frame.  Each frame is the frame rt_render_device gives. */
 rt_status rt_render_batch(rt_context* ctx, const rt_scene* scene, const rt_camera* cams,

@@ -40,7 +40,7 @@ enum PathKind : int {
 
 // Packet kernel frame batches (rt_render_batch): frames of one scene and launch shape, one per
 // blockIdx.z, each with its own camera position and the camera-dependent packet-image source.
-constexpr int kPkMaxBatch = 16;
+constexpr int kPkMaxBatch = 32;
 struct PkFrame {
     double cam[3];
     const double* img;         // cached LDS image of this camera, or null

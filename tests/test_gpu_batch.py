@@ -45,14 +45,14 @@ def _single(ds, pos, opts, rows, w):
 
 
 @pytest.mark.parametrize("name,w,h,n", [("c2", 480, 270, 1), ("c2", 480, 270, 5),
-                                        ("c2", 480, 270, 16), ("c2", 320, 180, 21),
+                                        ("c2", 480, 270, 16), ("c2", 320, 180, 21), ("c2", 160, 90, 35),
                                         ("c3", 480, 270, 6), ("c5", 320, 180, 4),
                                         ("c4", 400, 240, 3), ("mesh", 320, 180, 3),
                                         ("bigmesh", 320, 180, 3), ("mirror", 240, 160, 3),
                                         ("glass", 160, 120, 2)])
 def test_batch_frames_equal_single_renders(ctx, name, w, h, n):
     """Every frame of a batch equals rt_render_device of its camera, bit for bit (HDR and
-    Reinhard bytes): packet scenes in one launch per 16 frames (C2-C5, triangles), chain and
+    Reinhard bytes): packet scenes in one launch per 32 frames (C2-C5, triangles), chain and
     tree scenes one launch per frame.  Repeated, cached and first-seen cameras mixed."""
     sc = make_config(name, w, h)
     ds = ctx.scene(sc)
@@ -238,7 +238,7 @@ def test_gather_batch_rejects_gathered_and_local_output(ctx, comm1):
 
 
 @pytest.mark.parametrize("name,w,h,ranks,block,nf", [("c2", 480, 270, 8, 16, 4),
-                                                     ("c2", 160, 90, 3, 16, 18),  # 16 + 2 launches
+                                                     ("c2", 160, 90, 3, 16, 34),  # 32 + 2 frames per launch
                                                      ("c2", 480, 270, 3, 16, 5),
                                                      ("c3", 320, 180, 4, 8, 3),
                                                      ("c2", 200, 40, 4, 16, 2)])
@@ -284,7 +284,7 @@ def test_gather_all_batch_local_ranks_is_the_frames(name, w, h, ranks, block, nf
 @pytest.mark.parametrize("name,w,h,ranks,block,nf,weight", [
     ("c2", 480, 270, 8, 16, 4, 3), ("c2", 480, 270, 2, 16, 3, 2), ("c3", 320, 180, 4, 8, 3, 4),
     ("c2", 200, 40, 4, 16, 2, 2),   # some row sets empty
-    ("c2", 160, 90, 3, 16, 18, 2),  # 16 + 2 frames per row set
+    ("c2", 160, 90, 3, 16, 34, 2),  # 32 + 2 frames per row set
     ("glass", 160, 120, 3, 16, 2, 2)])
 def test_gather_all_batch_weighted_root_is_the_frames(name, w, h, ranks, block, nf, weight):
     """The weighted split (rt_comm_set_root_weight): the blocks dealt over weight + n − 1 row

@@ -2,7 +2,7 @@
 # GPU call (dev tool): the evidence of a round in one call.   bash tools/profile_round.sh TAG
 #   * the GPU test suite (-s: the parity tests print their byte-flip counts);
 #   * the default bench line, and rocprofv3 --kernel-trace --stats of the headline command;
-#   * rocprofv3 counter passes (tools/pmc_passes.sh) of the C2 batch launch (16 frames) and of the
+#   * rocprofv3 counter passes (tools/pmc_passes.sh) of the C2 batch launch (32 frames) and of the
 #     bigmesh triangle variant, incl. FETCH_SIZE / WRITE_SIZE for the HBM traffic;
 #   * the 8-rank row split with frames in flight (tools/inflight_balance.py).
 # Summaries afterwards: tools/valu_summary.py, tools/traffic_summary.py.  Every step has its own
@@ -25,7 +25,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/s
 find $OUT/stats -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 head -4 $OUT/kernel_stats.csv | cut -c1-160
 step pmc-c2
-timeout -k 10 500 bash tools/pmc_passes.sh $OUT/pmc_c2 c2 6 0 16 > $OUT/pmc_c2.log 2>&1 || { tail $OUT/pmc_c2.log; exit 1; }
+timeout -k 10 500 bash tools/pmc_passes.sh $OUT/pmc_c2 c2 6 0 32 > $OUT/pmc_c2.log 2>&1 || { tail $OUT/pmc_c2.log; exit 1; }
 step pmc-bigmesh
 timeout -k 10 500 bash tools/pmc_passes.sh $OUT/pmc_bigmesh bigmesh 10 > $OUT/pmc_bigmesh.log 2>&1 || { tail $OUT/pmc_bigmesh.log; exit 1; }
 step inflight
