@@ -605,8 +605,9 @@ def main(argv=None):
                 "kernel_ms_per_frame": round(mv["ranks"][0][0], 6),
                 "value": round(mv["rays"] * steps_x / mv["elapsed"] / 1e6, 3),
                 "note": "camera x moved by 1e-7 every frame: no frame reuses a cached per-camera "
-                        "packet image (each frame's first workgroup forms it and hands it to the "
-                        "later ones, DESIGN §4); rays counted at the first position"}
+                        "packet image (one small launch per batch forms every frame's image "
+                        "before the batch launch, DESIGN §4); rays counted at the first "
+                        "position"}
             sc1 = make_config("c1", aa=32)
             v, ms, k = single_launch_frames(R, sc1, 10, 2, capi.TONEMAPS.index("aces"))
             line["reference_main_c1"] = {

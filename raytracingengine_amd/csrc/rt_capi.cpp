@@ -465,6 +465,7 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
         st = packet_image(ctx, sc, p, flags, &rec);
         if (st != RT_OK) return st;
     }
+    int batch_ring = -1;  // the ring entry of this batch's formed images, if any
     if (packet && nframes > 1) {
         // a frame batch: frame f's camera and image source (cached image, hand-off slot, or
         // formed per workgroup); the tile order is the first frame's (it permutes tiles only)
@@ -487,6 +488,34 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
             F.pub = q.pk_pub;
             F.epoch = q.pk_epoch;
             F._pad = 0;
+        }
+        // frames without a cached image (first sightings: a moving camera) would each form
+        // theirs in the launch (hand-off slot or every workgroup); instead one small launch
+        // forms every frame's image into a ring entry first, read like a cached one
+        bool any_uncached = false;
+        for (int f = 0; f < nframes; ++f) any_uncached = any_uncached || !p.fr[f].img;
+        if (any_uncached && nframes >= 2) {
+            const size_t img_bytes = (packet_lds_bytes(p.ns, p.np, p.nl) + 255) & ~size_t(255);
+            const size_t entry = img_bytes * kPkMaxBatch;
+            RT_HIP(sc->pk_batch.ensure(entry * rt_scene::kPkBatchRing));
+            const int r = sc->pk_batch_next;
+            sc->pk_batch_next = (r + 1) % rt_scene::kPkBatchRing;
+            if (!sc->pk_batch_done[r])
+                RT_HIP(hipEventCreateWithFlags(&sc->pk_batch_done[r], hipEventDisableTiming));
+            if (sc->pk_batch_used[r])  // the batch that last read this entry, on any stream
+                RT_HIP(hipStreamWaitEvent(ctx->stream, sc->pk_batch_done[r], 0));
+            double* base = reinterpret_cast<double*>(static_cast<char*>(sc->pk_batch.ptr) +
+                                                     static_cast<size_t>(r) * entry);
+            RT_HIP(launch_packet_image_batch(p, nframes, base, img_bytes / sizeof(double),
+                                             ctx->stream));
+            for (int f = 0; f < nframes; ++f) {
+                PkFrame& F = p.fr[f];
+                if (F.img) continue;  // a cached image: the same words
+                F.img = base + static_cast<size_t>(f) * (img_bytes / sizeof(double));
+                F.pub = nullptr;
+                F.epoch = 0;
+            }
+            batch_ring = r;
         }
     }
     // generic kernels without triangle / area-light code for scenes that use neither
@@ -543,6 +572,10 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
         pc.counters = static_cast<unsigned long long*>(ctx->counters.ptr);
         pc.tile_cost = nullptr;  // the durations are the image launch's
         RT_HIP(launch(pc, true));
+    }
+    if (batch_ring >= 0) {  // the entry is free again once these launches have completed
+        RT_HIP(hipEventRecord(sc->pk_batch_done[batch_ring], ctx->stream));
+        sc->pk_batch_used[batch_ring] = true;
     }
     return scratch ? scratch_done(ctx) : RT_OK;
 }
@@ -819,6 +852,9 @@ rt_status rt_scene_destroy(rt_scene* sc) {
     (void)hipDeviceSynchronize();
     sc->buf.release();
     sc->pk_pub.release();
+    sc->pk_batch.release();
+    for (auto& e : sc->pk_batch_done)
+        if (e) (void)hipEventDestroy(e);
     for (auto& im : sc->pk_images) {
         im.buf.release();
         if (im.ready) (void)hipEventDestroy(im.ready);

@@ -131,6 +131,15 @@ struct rt_scene {
     // Cameras without an image: a ring of kPkPubSlots publish slots (rt_packet.hip, in-launch
     // image hand-off), each launch tagged with its own epoch; zeroed once at allocation.
     mutable rtamd::DeviceBuffer pk_pub;
+    // Frame batches with cameras that have no cached image (a moving camera): one small launch
+    // forms every frame's image into a ring entry of kPkBatchRing × kPkMaxBatch images before
+    // the batch launch, which copies them like cached ones; an entry is reused only after the
+    // batch that read it (its event) has completed.
+    static constexpr int kPkBatchRing = 4;
+    mutable rtamd::DeviceBuffer pk_batch;
+    mutable hipEvent_t pk_batch_done[kPkBatchRing] = {nullptr, nullptr, nullptr, nullptr};
+    mutable bool pk_batch_used[kPkBatchRing] = {false, false, false, false};
+    mutable int pk_batch_next = 0;
 };
 
 namespace rtamd {

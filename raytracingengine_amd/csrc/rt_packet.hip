@@ -1445,6 +1445,22 @@ hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t st
     return hipGetLastError();
 }
 
+// The images of a frame batch's cameras, one workgroup per frame (pk_build_image: the same
+// words a workgroup of the batch launch would form for itself).
+__global__ __launch_bounds__(256) void packet_image_batch_kernel(TraceParams P, double* img,
+                                                                 size_t stride) {
+    pk_build_image(P, P.fr[blockIdx.x].cam, img + blockIdx.x * stride,
+                   static_cast<int>(threadIdx.x), 256);
+}
+
+hipError_t launch_packet_image_batch(const TraceParams& p, int nframes, double* img,
+                                     size_t stride, hipStream_t stream) {
+    if (nframes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(packet_image_batch_kernel, dim3(static_cast<unsigned>(nframes)),
+                       dim3(256), 0, stream, p, img, stride);
+    return hipGetLastError();
+}
+
 int packet_max_spheres() { return 16 * 64; }
 
 void packet_grid(const TraceParams& p, uint32_t& gx, uint32_t& gy, uint32_t& waves) {
