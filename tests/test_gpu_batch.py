@@ -327,3 +327,41 @@ def test_gather_all_batch_weighted_root_is_the_frames(name, w, h, ranks, block, 
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_moving_batches_on_two_streams_reuse_the_image_ring(ctx):
+    """Batches of first-seen cameras (a camera that moves every frame) get every frame's packet
+    image formed by one small launch into a ring entry (rt_capi.cpp enqueue_frames, 4 entries)
+    that the batch launch reads like cached images.  Seven batches alternating between two
+    streams, enqueued without waiting, wrap the ring twice: every frame equals its single
+    render."""
+    sc = make_config("c2", 320, 180)
+    W, H, n = 320, 180, 4
+    ds = ctx.scene(sc)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    base = ds.camera["position"][0].copy()
+    try:
+        batches = [[base + (0.01 * (b * n + f + 1), -0.005 * f, 0.02 * b) for f in range(n)]
+                   for b in range(7)]
+        opts = capi.default_opts(tonemap=1)
+        outs = []
+        for b, pos in enumerate(batches):
+            ctx.set_stream(streams[b % 2].cuda_stream)
+            h = torch.empty(n * H * W * 3, dtype=torch.float64, device="cuda")
+            l = torch.empty(n * H * W * 3, dtype=torch.uint8, device="cuda")
+            ds.render_batch(ds.cameras(np.array(pos)), h.data_ptr(), None, l.data_ptr(), opts)
+            outs.append((h, l))
+        torch.cuda.synchronize()
+        ctx.set_stream(None)
+        for b, pos in enumerate(batches):
+            h, l = outs[b]
+            a64 = h.cpu().numpy().reshape(n, -1)
+            a8 = l.cpu().numpy().reshape(n, -1)
+            for f, p in enumerate(pos):
+                r64, r8 = _single(ds, p, capi.default_opts(tonemap=1), H, W)
+                assert np.array_equal(a64[f], r64), (b, f)
+                assert np.array_equal(a8[f], r8), (b, f)
+    finally:
+        ctx.set_stream(None)
+        ds.camera["position"][0] = base
+        ds.close()
