@@ -26,7 +26,7 @@ from raytracingengine_amd.distributed import render_opts_for, row_ranges
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 STREAMS = [int(s) for s in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "2", "3", "4"])]
 CONFIGS = sys.argv[3:] or ["c2"]
-BATCHES = [4, 8, 16]
+BATCHES = [4, 8, 16, 32]
 FRAMES = 240
 BLOCK = 16
 
