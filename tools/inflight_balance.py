@@ -9,7 +9,9 @@ first waits behind ~3 ms of whole frames on stream 0 (real work, so the GPU keep
 clock — a sleep kernel lets it drop), long enough to cover the host's enqueue of all F frames,
 so the launches reach the GPU back to back; the host's own enqueue cost per frame is reported
 beside it (`host_us`).  The full frame on one stream, measured the same way, is the reference:
-the target is a rank-frame <= 1.3 x full / ranks.
+the target is a rank-frame <= 1.3 x full / ranks.  `weighted`: rank 0's and the slowest peer's
+time per frame when rank 0 renders w of w + ranks − 1 row sets (rt_comm_set_root_weight), against
+bench.py choose_root_weight's model (T·w/V and T/V).
 """
 import json
 import sys
@@ -148,6 +150,25 @@ for name in CONFIGS:
         out.setdefault("batch_host_us", {})[G] = round(sum(hs) / n, 2)
         out.setdefault("batch_max_rank_over_full_div_n", {})[G] = round(max(ts) / (full[1][0] / n), 3)
         del bbufs
+    # the weighted split (rt_comm_set_root_weight): rank 0 renders w of the w + n − 1 row sets
+    # (one batch launch per set), every other rank one — measured per frame at 32-frame batches
+    G = 32
+    bbufs = [(torch.empty(G * W * H * 3, dtype=torch.float64, device="cuda"),
+              torch.empty(G * W * H * 3, dtype=torch.uint8, device="cuda")) for _ in range(2)]
+    Tb = out["batch_full_frame_ms"][G]
+    for w in (2, 3):
+        V = w + n - 1
+        slot_ms = []
+        for sl in range(V):
+            o = render_opts_for(row_ranges(sl, V, H, BLOCK), sl, V, H, BLOCK, tonemap=1)
+            warm(ds, o, bufs, 20)
+            g, _ = run_batch(ds, o, bbufs, G, max(4, FRAMES // G), cyc)
+            slot_ms.append(g)
+        out.setdefault("weighted", {})[w] = {
+            "sets": V, "rank0_ms": round(sum(slot_ms[:w]), 5),
+            "peer_max_ms": round(max(slot_ms[w:]), 5),
+            "model_rank0_ms": round(Tb * w / V, 5), "model_peer_ms": round(Tb / V, 5)}
+    del bbufs
     print(json.dumps(out), flush=True)
     ds.close()
 ctx.close()
