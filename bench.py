@@ -49,8 +49,9 @@ HDR_BYTES = {"f64": 24, "f32": 12}
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200, help="timed frames")
-    ap.add_argument("--warmup", type=int, default=20, help="untimed frames after the clock warm-up")
+    ap.add_argument("--steps", type=int, default=256,
+                    help="timed frames (default: 8 full batches of 32)")
+    ap.add_argument("--warmup", type=int, default=32, help="untimed frames after the clock warm-up")
     ap.add_argument("--config", default="c2",
                     help="c1..c5 (BASELINE configs), mirror, glass, mesh, bigmesh; default c2")
     ap.add_argument("--batch", type=int, default=32,
