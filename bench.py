@@ -43,6 +43,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
+FP64_VALU_PEAK_TF = 78.6  # FP64 vector FMA-counted peak (1024 SIMDs x 2.4 GHz x 32)
 HDR_BYTES = {"f64": 24, "f32": 12}
 
 
@@ -62,10 +63,11 @@ def parse_args(argv=None):
                     help="rows per block of the block-cyclic split (N>1)")
     ap.add_argument("--hdr", choices=["f64", "f32"], default="f64",
                     help="the rank-local HDR framebuffer: f64 = the reference's std::vector<Vec3>")
-    ap.add_argument("--root-weight", default="auto",
+    ap.add_argument("--root-weight", default="1",
                     help="N>1: rank 0's share of the row split (rt_comm_set_root_weight): an "
-                         "integer, or 'auto' = chosen from an untimed equal-split probe of the "
-                         "ranks' render and gather times (1 unless the gathers are link-bound)")
+                         "integer (default 1: the equal split), or 'auto' = chosen from an "
+                         "untimed equal-split probe of the ranks' render and gather times (opt-in: "
+                         "the weighted P2P path has not run on a multi-GPU node yet, DESIGN §6)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="gather on the render stream (no overlap of batch b's gather with "
                          "batch b+1's render)")
@@ -216,14 +218,19 @@ class Runner:
         self.dist.all_gather(out, t)
         return [[float(x) for x in o] for o in out]
 
-    def timed(self, step, frames, warmup, batch, warm_step=None, region_events=False):
+    def timed(self, step, frames, warmup, batch, warm_step=None, region_events=False,
+              sync=None):
         """Untimed work for `--clock-warmup-ms` of wall time (the GPU leaves its idle clock only
         after ~30 ms of sustained load: tools/clock_ramp.py, C2 143 → 54 → 45 µs/frame over the
         first 30 ms), then `warmup` untimed frames, then `frames` timed frames between barrier +
         synchronize.  step(first_frame, nframes, timed) enqueues nframes frames (≤ batch).
         Returns (elapsed seconds max over ranks, HIP-event region ms on the launch stream).
         `warm_step` (default `step`) is what the clock warm-up runs: it must not be a
-        collective, since each rank warms up for its own wall time."""
+        collective, since each rank warms up for its own wall time.  Frame indices (what a
+        moving camera derives its position from) run on across the phases: the warmup has
+        [0, warmup), the timed frames [warmup, warmup + frames), so no timed frame revisits a
+        warmup position.  `sync` (the communicator's deadline-guarded wait) runs before the
+        device synchronisation that closes the timed region."""
         torch = self.torch
         warm = warm_step or step
         t_end = time.perf_counter() + self.args.clock_warmup_ms / 1e3
@@ -234,9 +241,9 @@ class Runner:
                 k += batch
             torch.cuda.synchronize()
 
-        def run(n, timed):
+        def run(n, timed, first=0):
             for f0 in range(0, n, batch):
-                step(f0, min(batch, n - f0), timed)
+                step(first + f0, min(batch, n - f0), timed)
 
         run(warmup, False)
         # drain this rank's work (its RCCL gathers included) before the process group's own
@@ -247,8 +254,10 @@ class Runner:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(self.stream)   # on the stream the trace kernel is launched on
-        run(frames, True)
+        run(frames, True, first=warmup)
         ev1.record(self.stream)
+        if sync is not None:
+            sync()
         torch.cuda.synchronize()
         self.barrier()
         elapsed = time.perf_counter() - t0
@@ -359,7 +368,7 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
                               flags=pf | capi.RT_FLAG_TIME_KERNEL)
     base = dscene.camera["position"][0].copy()
     static_cams = dscene.cameras([base] * batch)
-    nb, nt = [0], [0]
+    nb, nt, nev = [0], [0], [0]
 
     def cams_for(f0, n):
         if camera_step is None:
@@ -373,6 +382,8 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
         ev = timed and event_every > 0 and nt[0] % event_every == 0
         if timed:
             nt[0] += 1
+        if ev:
+            nev[0] += 1
         kw = {"rank_hdr64": local[b & 1].data_ptr()} if hdr == "f64" else \
              {"rank_hdr32": local[b & 1].data_ptr()}
         comm.render_gather_batch(dscene, cams_for(f0, n), topts if ev else opts, capi.RT_OUT_LDR,
@@ -391,12 +402,14 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
                                 ldr[0].data_ptr() if root else local[1].data_ptr(), wopts)
 
     comm.timing(reset=True)
-    elapsed, _ = R.timed(step, frames, warmup, batch, warm_step=warm_step if split else None)
+    elapsed, _ = R.timed(step, frames, warmup, batch, warm_step=warm_step if split else None,
+                         sync=comm.synchronize if split else None)
     t = comm.timing(reset=True)
     if split and weight != 1:
         comm.set_root_weight(1)
     per_frame = [t.render_ms / max(t.frames, 1), t.gather_ms / max(t.frames, 1),
-                 t.assemble_ms / max(t.frames, 1), float(rows), float(rays_rank), float(t.frames)]
+                 t.assemble_ms / max(t.frames, 1), float(rows), float(rays_rank), float(t.frames),
+                 float(nev[0]), t.render_ms]
     ranks = R.gather_rows(per_frame)
     (rays_all,) = R.sum_over_ranks(float(rays_rank))
     dscene.close()
@@ -523,10 +536,22 @@ def main(argv=None):
     r0 = res["ranks"][0]
     # the trace kernel: rank 0's render per frame (HIP events around each timed batch launch)
     render_ms = r0[0]
+    ev_launches = max(int(r0[6]), 1)
+    frames_per_launch = r0[5] / ev_launches      # the frames the event-timed launches held
+    launch_ms = r0[7] / ev_launches               # measured per launch, not render_ms x batch
     bytes_per_frame = int(r0[3]) * W * (HDR_BYTES[args.hdr] + 3)
     achieved = bytes_per_frame / (render_ms / 1e3) / 1e9 if render_ms > 0 else 0.0
-    # PMC traffic of the batch launch (tools/pmc_passes.sh with the bench's batch), per launch
-    traffic, traffic_src = load_profile(f"pmc_{args.config}_batch{batch}.json")
+    # §8(d)'s FLOP roofline: F_ray = 25·Ns + 14·Np FP64 flops per ray of the reference's
+    # brute-force IntersectClosest, rank 0's rays per frame / its render time per frame
+    f_ray = 25 * len(sc.spheres) + 14 * len(sc.planes)
+    flops_frame = res["rays_rank"] * f_ray if R.world == 1 else r0[4] * f_ray
+    flops_tf = flops_frame / (render_ms / 1e3) / 1e12 if render_ms > 0 else 0.0
+    # PMC traffic of a 32-frame batch launch (tools/pmc_passes.sh), scaled per frame to the
+    # frames the timed launch held
+    traffic, traffic_src = load_profile(f"pmc_{args.config}_batch32.json")
+    traffic_launch = None
+    if traffic and R.world == 1:
+        traffic_launch = traffic["hbm_bytes_per_launch"] / 32 * frames_per_launch
     valu, valu_src = load_profile(f"r04_{args.config}_valu.json")
     if valu is None:
         valu, valu_src = load_profile(f"r03_{args.config}_valu.json")
@@ -554,19 +579,30 @@ def main(argv=None):
         "root_weight_probe": probe,
         "clock_warmup_ms": args.clock_warmup_ms,
         "kernel_ms_per_frame": round(render_ms, 6),
-        "kernel_ms_per_launch": round(render_ms * batch, 6),
+        "kernel_ms_per_launch": round(launch_ms, 6),
+        "frames_per_timed_launch": round(frames_per_launch, 3),
         **summ,
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": (traffic.get("hbm_bytes_per_launch") if traffic and R.world == 1
-                        else None),
-            "alg_bytes_per_launch": bytes_per_frame * batch,
+            "traffic": round(traffic_launch) if traffic_launch else None,
+            "alg_bytes_per_launch": round(bytes_per_frame * frames_per_launch),
             "alg_bytes_per_frame": bytes_per_frame,
             "traffic_source": traffic_src if R.world == 1 else None,
+            "traffic_note": ("PMC FETCH_SIZE x2 + WRITE_SIZE of a 32-frame launch of this "
+                             "config (committed summary), per frame x the frames of the timed "
+                             "launch") if traffic_launch else None,
+            "flops_alg_per_frame": flops_frame,
+            "flops_alg_tflops": round(flops_tf, 3),
+            "flops_alg_frac": round(flops_tf / FP64_VALU_PEAK_TF, 5),
+            "flops_note": (f"SURVEY §8(d): rays x F_ray (25*Ns + 14*Np = {f_ray} FP64 flops of "
+                           "the reference's brute-force IntersectClosest per ray) / render time "
+                           f"/ {FP64_VALU_PEAK_TF} TF; culling skips most of that work, so this "
+                           "is the reference algorithm's rate, not counted flops (valu)"),
             "note": "rank 0's batch launch: its rows' framebuffer bytes (HDR + u8) per frame / "
                     "its render time per frame (HIP events around every "
-                    f"{args.event_every}-th timed batch launch of {batch} frames)",
+                    f"{args.event_every}-th timed batch launch; those launches held "
+                    f"{frames_per_launch:g} frames each)",
         },
         "valu": valu if R.world == 1 else None,
         "valu_source": valu_src if R.world == 1 else None,
@@ -617,6 +653,20 @@ def main(argv=None):
                 "ms_per_frame": round(ms, 4), "kernel_ms_per_launch": round(k, 4),
                 "value": round(v, 3), "unit": "Mrays/s"}
             line["d2h"] = d2h_frames(R, sc, min(args.steps, 20), tonemap)
+        # BASELINE config 3 (SURVEY §8e asks for scaling runs on C2, C3 and C4): the 4K frame,
+        # 128 spheres, 4 point lights, row-tiled through the same path
+        sc3 = make_config("c3", aa=1)
+        n3 = min(args.steps, 32)
+        t3 = split_frames(R, sc3, n3, min(args.warmup, 8), 8, "f64", tonemap, args.row_block,
+                          not args.no_pipeline, 1)
+        line["c3_tiled"] = {
+            "value": round(t3["rays"] * n3 / t3["elapsed"] / 1e6, 3),
+            "ms_per_frame": round(t3["elapsed"] / n3 * 1e3, 5),
+            "frames": n3,
+            "workload": "c3 3840x2160, 128 spheres, 4 planes, 4 point lights, f64 HDR rows on "
+                        "each rank + Reinhard u8 gathered, 8 frames per call",
+            **per_rank_summary(t3)}
+        del t3
         # BASELINE config 4: the 8K frame row-tiled through the same path
         sc4 = make_config("c4", aa=1)
         t4 = split_frames(R, sc4, min(args.steps, 16), min(args.warmup, 2), 2, "f64", tonemap,

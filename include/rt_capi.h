@@ -252,9 +252,21 @@ typedef struct rt_gather_timing {
 
 /* ncclGetUniqueId: called on one process, the bytes handed to every rank (any transport). */
 rt_status rt_comm_unique_id(uint8_t* id /* RT_COMM_ID_BYTES */);
-/* One rank of an n-rank communicator on ctx's device (ncclCommInitRank): one process per GPU.
- * Destroy communicators before their contexts. */
+/* One rank of an n-rank communicator on ctx's device (non-blocking ncclCommInitRankConfig): one
+ * process per GPU.  Destroy communicators before their contexts.  Failure detection (SURVEY §5;
+ * the reference has no communicator): every wait on the communicator — its initialisation, the
+ * issue of each gather, rt_comm_synchronize, rt_comm_set_root_weight — polls
+ * ncclCommGetAsyncError with a deadline (rt_comm_create: RTAMD_COMM_TIMEOUT_MS, default 300000;
+ * 0 = none).  On an asynchronous RCCL error or at the deadline the communicator is aborted
+ * (ncclCommAbort: its kernels in flight return) and the call fails with RT_ERR_RCCL; every later
+ * call on it fails the same way (destroy it and create a new one).  A rank whose peers never
+ * join therefore gets RT_ERR_RCCL from rt_comm_create instead of blocking for ever. */
 rt_status rt_comm_create(rt_context* ctx, int nranks, int rank, const uint8_t* id, rt_comm** out);
+/* rt_comm_create with its deadline in milliseconds (0 = wait without a deadline). */
+rt_status rt_comm_create_ex(rt_context* ctx, int nranks, int rank, const uint8_t* id,
+                            long timeout_ms, rt_comm** out);
+/* The deadline of the communicator's later waits (milliseconds, 0 = none). */
+rt_status rt_comm_set_timeout(rt_comm* comm, long timeout_ms);
 /* n communicators, one per context, over n DISTINCT devices from one process (ncclCommInitAll);
  * comms_out[i] is rank i on ctxs[i]. */
 rt_status rt_comm_create_all(rt_context* const* ctxs, int n, rt_comm** comms_out);
@@ -267,7 +279,9 @@ rt_status rt_comm_create_local(rt_context* const* ctxs, int n, rt_comm** comms_o
 rt_status rt_comm_destroy(rt_comm* comm);
 rt_status rt_comm_info(const rt_comm* comm, int* nranks, int* rank);
 /* Weighted row split (every rank of the communicator sets the same weight before its next frame;
- * default 1): the frame's blocks are dealt over weight + n − 1 row sets, rank 0 renders `weight`
+ * default 1).  Collective on an rt_comm_create communicator with n > 1: the ranks check that
+ * they agree (one all-reduce) and all return RT_ERR_INVALID_ARG, weight unchanged, if not.
+ * rt_render_gather_all[_batch] checks that its communicators carry one weight.  The frame's blocks are dealt over weight + n − 1 row sets, rank 0 renders `weight`
  * of them and every other rank one — rank 0's rows never cross a link, so when the peers' gathers
  * are link-bound it takes a larger share.  With weight > 1 the gather is a group of P2P sends of
  * equal counts (ncclSend / ncclRecv) into rank 0's receive buffer, where rank 0 renders its own
@@ -306,7 +320,9 @@ rt_status rt_render_gather_all_batch(rt_comm* const* comms, rt_scene* const* sce
                                      const rt_camera* cams, int nframes,
                                      const rt_render_opts* opts, int outputs, void* d_hdr64,
                                      void* d_hdr32, void* d_ldr);
-/* Waits for every frame enqueued on the communicator (render, gather, assembly). */
+/* Waits for every frame enqueued on the communicator (render, gather, assembly); on an
+ * rt_comm_create communicator with n > 1 it polls the streams and ncclCommGetAsyncError and
+ * aborts the communicator on an RCCL error or at its deadline (RT_ERR_RCCL). */
 rt_status rt_comm_synchronize(rt_comm* comm);
 /* Summed frame timings since the last reset (waits for the timed frames to finish). */
 rt_status rt_comm_timing(rt_comm* comm, rt_gather_timing* out, int reset);

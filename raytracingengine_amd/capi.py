@@ -41,7 +41,8 @@ EXPORTED = [
     "rt_context_destroy", "rt_context_set_stream", "rt_context_synchronize", "rt_scene_create",
     "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
     "rt_render_multi", "rt_comm_unique_id", "rt_comm_create", "rt_comm_create_all",
-    "rt_comm_create_local", "rt_comm_destroy", "rt_comm_info", "rt_comm_set_root_weight", "rt_render_gather", "rt_render_gather_all",
+    "rt_comm_create_local", "rt_comm_destroy", "rt_comm_info", "rt_comm_set_root_weight",
+    "rt_comm_create_ex", "rt_comm_set_timeout", "rt_render_gather", "rt_render_gather_all",
     "rt_comm_timing", "rt_comm_synchronize", "rt_debug_assemble_rows", "rt_debug_tile_order",
     "rt_stats_read", "rt_stats_reset", "rt_trace_rays", "rt_intersect_rays", "rt_tonemap",
     "rt_debug_f64_ops", "rt_debug_vec_ops", "rt_queue_create", "rt_queue_destroy",
@@ -134,6 +135,8 @@ def load_library(path: str = LIB_PATH):
         "rt_debug_vec_ops": [vp, vp, ctypes.c_size_t, vp],
         "rt_comm_unique_id": [vp],
         "rt_comm_create": [vp, i32, i32, vp, vp],
+        "rt_comm_create_ex": [vp, i32, i32, vp, ctypes.c_long, vp],
+        "rt_comm_set_timeout": [vp, ctypes.c_long],
         "rt_comm_create_all": [vp, i32, vp],
         "rt_comm_create_local": [vp, i32, vp],
         "rt_comm_destroy": [vp],
@@ -459,7 +462,10 @@ class Comm:
     """One rank of a row-tiled multi-GPU frame (rt_comm): render this rank's rows, one RCCL
     gather to rank 0, assembled into rank 0's device framebuffers (rt_render_gather)."""
 
-    def __init__(self, ctx: Context, nranks: int, rank: int, uid: bytes, _handle=None):
+    def __init__(self, ctx: Context, nranks: int, rank: int, uid: bytes, _handle=None,
+                 timeout_ms: int | None = None):
+        """timeout_ms: the deadline of the communicator's waits (rt_comm_create_ex; None = the
+        library default, RTAMD_COMM_TIMEOUT_MS or 300 s; 0 = none)."""
         L = load_library()
         self.ctx = ctx
         self.nranks, self.rank = nranks, rank
@@ -471,7 +477,11 @@ class Comm:
             raise ValueError("unique id must be RT_COMM_ID_BYTES bytes")
         idbuf = (ctypes.c_uint8 * RT_COMM_ID_BYTES).from_buffer_copy(uid)
         with _StdoutToStderr():
-            st = L.rt_comm_create(ctx.handle, nranks, rank, idbuf, ctypes.byref(self._h))
+            if timeout_ms is None:
+                st = L.rt_comm_create(ctx.handle, nranks, rank, idbuf, ctypes.byref(self._h))
+            else:
+                st = L.rt_comm_create_ex(ctx.handle, nranks, rank, idbuf, int(timeout_ms),
+                                         ctypes.byref(self._h))
         _check(st)
 
     @classmethod
@@ -532,6 +542,9 @@ class Comm:
 
     def synchronize(self):
         _check(_lib.rt_comm_synchronize(self._h))
+
+    def set_timeout(self, timeout_ms: int):
+        _check(_lib.rt_comm_set_timeout(self._h, int(timeout_ms)))
 
     def set_root_weight(self, weight: int):
         """Weighted row split (rt_comm_set_root_weight): rank 0 renders `weight` of the

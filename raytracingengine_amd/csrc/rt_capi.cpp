@@ -262,8 +262,10 @@ rt_status packet_publish_slot(rt_context* ctx, const rt_scene* sc, TraceParams& 
 // workgroup renders which tile: every pixel is computed by the same instructions, so images do
 // not change (RT_FLAG_NO_TILE_ORDER: the default order, for A/B runs and the tests).  `*rec`
 // receives the entry whose recording launch enqueue_render marks complete.
+// existing_only: use an order already built for this shape, never record or build one (frame
+// batches with several cameras: their launch neither pays the recording nor waits on a build).
 rt_status tile_order(rt_context* ctx, rt_scene::PkImage& im, TraceParams& p, int flags,
-                     rt_scene::PkImage::TileOrder** rec) {
+                     rt_scene::PkImage::TileOrder** rec, bool existing_only = false) {
     *rec = nullptr;
     if (flags & RT_FLAG_NO_TILE_ORDER) return RT_OK;
     uint32_t gx, gy, waves;
@@ -273,6 +275,7 @@ rt_status tile_order(rt_context* ctx, rt_scene::PkImage& im, TraceParams& p, int
     const uint32_t tiles = gx * gy;
     size_t idx = 0;
     while (idx < im.ords.size() && std::memcmp(im.ords[idx].key, key, sizeof key) != 0) ++idx;
+    if (existing_only && (idx == im.ords.size() || im.ords[idx].state != 2)) return RT_OK;
     if (idx == im.ords.size()) {  // a new launch shape: record this launch
         if (im.ords.size() >= kMaxTileOrders) return RT_OK;  // the default order
         if (im.ords.capacity() < kMaxTileOrders) im.ords.reserve(kMaxTileOrders);
@@ -317,49 +320,188 @@ rt_status tile_order(rt_context* ctx, rt_scene::PkImage& im, TraceParams& p, int
     return RT_OK;
 }
 
-rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p, int flags,
-                       rt_scene::PkImage::TileOrder** rec) {
-    *rec = nullptr;
+// The cached image of this camera position, or null; a render on another stream than the one
+// that formed it waits for the entry's event until it has completed.
+rt_status packet_image_cached(rt_context* ctx, const rt_scene* sc, const double* cam,
+                              rt_scene::PkImage** out) {
+    *out = nullptr;
     for (auto& im : sc->pk_images) {
-        if (std::memcmp(im.cam, p.cam_pos, sizeof im.cam) != 0) continue;
+        if (std::memcmp(im.cam, cam, sizeof im.cam) != 0) continue;
         if (!im.done && im.stream != ctx->stream) {
             const hipError_t q = hipEventQuery(im.ready);
             if (q == hipSuccess) im.done = true;
             else if (q == hipErrorNotReady) RT_HIP(hipStreamWaitEvent(ctx->stream, im.ready, 0));
             else return hip_fail(q, "hipEventQuery");
         }
-        p.pk_image = static_cast<const double*>(im.buf.ptr);
-        return tile_order(ctx, im, p, flags, rec);
+        *out = &im;
+        return RT_OK;
     }
+    return RT_OK;
+}
+
+// A camera without a cached image: true when it was seen before (the last kMaxPkSeen first
+// sightings) and the cache has room, i.e. it should get a cache entry now (removed from the seen
+// list); otherwise it is remembered as seen once.
+bool packet_second_sighting(const rt_scene* sc, const double* cam) {
     auto& seen = sc->pk_seen;
     auto it = std::find_if(seen.begin(), seen.end(), [&](const std::array<double, 3>& c) {
-        return std::memcmp(c.data(), p.cam_pos, sizeof p.cam_pos) == 0;
+        return std::memcmp(c.data(), cam, 3 * sizeof(double)) == 0;
     });
-    if (it == seen.end()) {  // first sighting: remember it, no setup launch
+    if (it == seen.end()) {
         if (seen.size() >= kMaxPkSeen) seen.erase(seen.begin());
-        seen.push_back({p.cam_pos[0], p.cam_pos[1], p.cam_pos[2]});
-        return packet_publish_slot(ctx, sc, p);
+        seen.push_back({cam[0], cam[1], cam[2]});
+        return false;
     }
-    if (sc->pk_images.size() >= kMaxPkImages) return packet_publish_slot(ctx, sc, p);
+    if (sc->pk_images.size() >= kMaxPkImages) return false;
     seen.erase(it);
+    return true;
+}
+
+// A new cache entry for this camera (its buffer allocated, its event created; the caller
+// enqueues the launch that forms the image and records `ready` after it on ctx->stream).
+rt_status packet_image_entry(rt_context* ctx, const rt_scene* sc, const double* cam,
+                             const TraceParams& p, rt_scene::PkImage** out) {
+    *out = nullptr;
     // never reallocated: a frame batch holds entries of earlier frames while adding one
     if (sc->pk_images.capacity() < kMaxPkImages) sc->pk_images.reserve(kMaxPkImages);
     sc->pk_images.emplace_back();
     rt_scene::PkImage& im = sc->pk_images.back();
-    std::memcpy(im.cam, p.cam_pos, sizeof im.cam);
+    std::memcpy(im.cam, cam, sizeof im.cam);
     im.stream = ctx->stream;
     hipError_t e = im.buf.ensure(packet_lds_bytes(p.ns, p.np, p.nl));
     if (e == hipSuccess) e = hipEventCreateWithFlags(&im.ready, hipEventDisableTiming);
-    if (e == hipSuccess) e = launch_packet_image(p, static_cast<double*>(im.buf.ptr), ctx->stream);
-    if (e == hipSuccess) e = hipEventRecord(im.ready, ctx->stream);
     if (e != hipSuccess) {
         im.buf.release();
         if (im.ready) (void)hipEventDestroy(im.ready);
         sc->pk_images.pop_back();
+        return hip_fail(e, "packet image entry");
+    }
+    *out = &im;
+    return RT_OK;
+}
+
+// One-frame launches: the cached image; on a camera's second sighting a one-workgroup setup
+// launch forms its cache entry; on a first sighting a publish slot.
+rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p, int flags,
+                       rt_scene::PkImage::TileOrder** rec) {
+    *rec = nullptr;
+    rt_scene::PkImage* found = nullptr;
+    rt_status st = packet_image_cached(ctx, sc, p.cam_pos, &found);
+    if (st != RT_OK) return st;
+    if (found) {
+        p.pk_image = static_cast<const double*>(found->buf.ptr);
+        return tile_order(ctx, *found, p, flags, rec);
+    }
+    if (!packet_second_sighting(sc, p.cam_pos)) return packet_publish_slot(ctx, sc, p);
+    rt_scene::PkImage* im = nullptr;
+    st = packet_image_entry(ctx, sc, p.cam_pos, p, &im);
+    if (st != RT_OK) return st;
+    hipError_t e = launch_packet_image(p, static_cast<double*>(im->buf.ptr), ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(im->ready, ctx->stream);
+    if (e != hipSuccess) {
+        im->buf.release();
+        (void)hipEventDestroy(im->ready);
+        sc->pk_images.pop_back();
         return hip_fail(e, "packet image setup");
     }
-    p.pk_image = static_cast<const double*>(im.buf.ptr);
-    return tile_order(ctx, im, p, flags, rec);
+    p.pk_image = static_cast<const double*>(im->buf.ptr);
+    return tile_order(ctx, *im, p, flags, rec);
+}
+
+// A frame batch's image sources (p.fr[f].img for every frame, before the batch launch): a
+// cached image, or one formed by ONE small launch for every frame that has none — into a new
+// cache entry when the camera was seen before (so a revisited position costs no launch of its
+// own), else into the batch's ring slot (an entry of kPkBatchRing, reused once the launches that
+// read it have completed).  Frames with the camera of an earlier frame of the batch share its
+// image.  The tile order: frame 0's, recorded / built only when every frame has frame 0's
+// camera (a static camera), otherwise only an order built earlier for the shape.
+rt_status packet_batch_images(rt_context* ctx, const rt_scene* sc, const rt_camera* cams,
+                              int nframes, TraceParams& p, int flags,
+                              rt_scene::PkImage::TileOrder** rec, int* batch_ring) {
+    *rec = nullptr;
+    *batch_ring = -1;
+    enum Kind { kCached, kPromote, kRing, kDup };
+    Kind kind[kPkMaxBatch];
+    int dup_of[kPkMaxBatch];
+    rt_scene::PkImage* ent[kPkMaxBatch] = {};
+    bool same_cam = true;
+    bool any_ring = false;
+    const size_t cache_before = sc->pk_images.size();
+    for (int f = 0; f < nframes; ++f) {
+        PkFrame& F = p.fr[f];
+        for (int i = 0; i < 3; ++i) F.cam[i] = cams[f].position[i];
+        F.img = nullptr;
+        F.pub = nullptr;
+        F.epoch = 0;
+        F._pad = 0;
+        if (std::memcmp(F.cam, p.fr[0].cam, sizeof F.cam) != 0) same_cam = false;
+        int g = 0;
+        while (g < f && std::memcmp(p.fr[g].cam, F.cam, sizeof F.cam) != 0) ++g;
+        if (g < f) {
+            kind[f] = kDup;
+            dup_of[f] = g;
+            continue;
+        }
+        rt_status st = packet_image_cached(ctx, sc, F.cam, &ent[f]);
+        if (st != RT_OK) return st;
+        if (ent[f]) {
+            kind[f] = kCached;
+            F.img = static_cast<const double*>(ent[f]->buf.ptr);
+            continue;
+        }
+        if (packet_second_sighting(sc, F.cam)) {
+            st = packet_image_entry(ctx, sc, F.cam, p, &ent[f]);
+            if (st != RT_OK) return st;
+            kind[f] = kPromote;
+            F.img = static_cast<const double*>(ent[f]->buf.ptr);
+            continue;
+        }
+        kind[f] = kRing;
+        any_ring = true;
+    }
+    const size_t img_doubles = ((packet_lds_bytes(p.ns, p.np, p.nl) + 255) & ~size_t(255)) /
+                               sizeof(double);
+    double* ring = nullptr;
+    if (any_ring) {
+        const size_t entry = img_doubles * sizeof(double) * kPkMaxBatch;
+        RT_HIP(sc->pk_batch.ensure(entry * rt_scene::kPkBatchRing));
+        const int r = sc->pk_batch_next;
+        sc->pk_batch_next = (r + 1) % rt_scene::kPkBatchRing;
+        if (!sc->pk_batch_done[r])
+            RT_HIP(hipEventCreateWithFlags(&sc->pk_batch_done[r], hipEventDisableTiming));
+        if (sc->pk_batch_used[r])  // the batch that last read this entry, on any stream
+            RT_HIP(hipStreamWaitEvent(ctx->stream, sc->pk_batch_done[r], 0));
+        ring = reinterpret_cast<double*>(static_cast<char*>(sc->pk_batch.ptr) +
+                                         static_cast<size_t>(r) * entry);
+        *batch_ring = r;
+    }
+    PkImageJobs jobs;
+    std::memset(&jobs, 0, sizeof jobs);
+    for (int f = 0; f < nframes; ++f) {
+        PkFrame& F = p.fr[f];
+        if (kind[f] == kRing) F.img = ring + static_cast<size_t>(f) * img_doubles;
+        if (kind[f] == kDup) F.img = p.fr[dup_of[f]].img;
+        if (kind[f] == kRing || kind[f] == kPromote) {
+            jobs.dst[jobs.n] = const_cast<double*>(F.img);
+            jobs.frame[jobs.n] = f;
+            ++jobs.n;
+        }
+    }
+    hipError_t e = launch_packet_image_batch(p, jobs, ctx->stream);
+    for (int f = 0; f < nframes && e == hipSuccess; ++f)
+        if (kind[f] == kPromote) e = hipEventRecord(ent[f]->ready, ctx->stream);
+    if (e != hipSuccess) {
+        // the entries this call created never received their image: drop them (newest last)
+        while (sc->pk_images.size() > cache_before) {
+            auto& im = sc->pk_images.back();
+            im.buf.release();
+            if (im.ready) (void)hipEventDestroy(im.ready);
+            sc->pk_images.pop_back();
+        }
+        return hip_fail(e, "packet batch images");
+    }
+    if (kind[0] == kCached) return tile_order(ctx, *ent[0], p, flags, rec, !same_cam);
+    return RT_OK;
 }
 
 // Whether a render of this TraceRay shape takes the breadth-first path, whose arena (ctx->wf,
@@ -461,62 +603,17 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
     // Scenes without secondary rays take the packet-culled kernel when its LDS image fits.
     const bool packet = packet_path;
     rt_scene::PkImage::TileOrder* rec = nullptr;  // set: this launch records wave durations
-    if (packet) {
-        st = packet_image(ctx, sc, p, flags, &rec);
-        if (st != RT_OK) return st;
-    }
     int batch_ring = -1;  // the ring entry of this batch's formed images, if any
     if (packet && nframes > 1) {
-        // a frame batch: frame f's camera and image source (cached image, hand-off slot, or
-        // formed per workgroup); the tile order is the first frame's (it permutes tiles only)
+        // a frame batch: frame f's camera and image source, all formed before the launch by at
+        // most one small launch (packet_batch_images)
         p.nframes = static_cast<uint32_t>(nframes);
         p.frame_px = frame_px;
-        for (int f = 0; f < nframes; ++f) {
-            TraceParams q = p;
-            if (f > 0) {
-                q.pk_image = nullptr;
-                q.pk_pub = nullptr;
-                q.pk_epoch = 0;
-                for (int i = 0; i < 3; ++i) q.cam_pos[i] = cams[f].position[i];
-                rt_scene::PkImage::TileOrder* unused = nullptr;
-                st = packet_image(ctx, sc, q, flags | RT_FLAG_NO_TILE_ORDER, &unused);
-                if (st != RT_OK) return st;
-            }
-            PkFrame& F = p.fr[f];
-            for (int i = 0; i < 3; ++i) F.cam[i] = q.cam_pos[i];
-            F.img = q.pk_image;
-            F.pub = q.pk_pub;
-            F.epoch = q.pk_epoch;
-            F._pad = 0;
-        }
-        // frames without a cached image (first sightings: a moving camera) would each form
-        // theirs in the launch (hand-off slot or every workgroup); instead one small launch
-        // forms every frame's image into a ring entry first, read like a cached one
-        bool any_uncached = false;
-        for (int f = 0; f < nframes; ++f) any_uncached = any_uncached || !p.fr[f].img;
-        if (any_uncached && nframes >= 2) {
-            const size_t img_bytes = (packet_lds_bytes(p.ns, p.np, p.nl) + 255) & ~size_t(255);
-            const size_t entry = img_bytes * kPkMaxBatch;
-            RT_HIP(sc->pk_batch.ensure(entry * rt_scene::kPkBatchRing));
-            const int r = sc->pk_batch_next;
-            sc->pk_batch_next = (r + 1) % rt_scene::kPkBatchRing;
-            if (!sc->pk_batch_done[r])
-                RT_HIP(hipEventCreateWithFlags(&sc->pk_batch_done[r], hipEventDisableTiming));
-            if (sc->pk_batch_used[r])  // the batch that last read this entry, on any stream
-                RT_HIP(hipStreamWaitEvent(ctx->stream, sc->pk_batch_done[r], 0));
-            double* base = reinterpret_cast<double*>(static_cast<char*>(sc->pk_batch.ptr) +
-                                                     static_cast<size_t>(r) * entry);
-            RT_HIP(launch_packet_image_batch(p, nframes, base, img_bytes / sizeof(double),
-                                             ctx->stream));
-            for (int f = 0; f < nframes; ++f) {
-                PkFrame& F = p.fr[f];
-                if (F.img) continue;  // a cached image: the same words
-                F.img = base + static_cast<size_t>(f) * (img_bytes / sizeof(double));
-                F.pub = nullptr;
-                F.epoch = 0;
-            }
-            batch_ring = r;
-        }
+        st = packet_batch_images(ctx, sc, cams, nframes, p, flags, &rec, &batch_ring);
+        if (st != RT_OK) return st;
+    } else if (packet) {
+        st = packet_image(ctx, sc, p, flags, &rec);
+        if (st != RT_OK) return st;
     }
     // generic kernels without triangle / area-light code for scenes that use neither
     const bool lean_generic = p.nt == 0 && p.al_samples == 0;
@@ -938,11 +1035,17 @@ rt_status rt_render(rt_context* ctx, const rt_scene* sc, const rt_camera* cam,
                               hipMemcpyDeviceToHost, ctx->stream));
     if (hldr)
         RT_HIP(hipMemcpyAsync(hldr, ctx->ldr.ptr, npx * 3, hipMemcpyDeviceToHost, ctx->stream));
+    unsigned long long c[2] = {0, 0};
+    if (stats) {
+        // the read-back is the counters' last use: a counting render queued on another stream
+        // waits for it (scratch_event), not only for the counting launch
+        RT_HIP(hipMemcpyAsync(c, ctx->counters.ptr, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
+        st = scratch_done(ctx);
+        if (st != RT_OK) return st;
+    }
     RT_HIP(hipStreamSynchronize(ctx->stream));
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
-        unsigned long long c[2] = {0, 0};
-        RT_HIP(hipMemcpy(c, ctx->counters.ptr, sizeof c, hipMemcpyDeviceToHost));
         stats->trace_rays = c[0];
         stats->shadow_rays = c[1];
         if (o.flags & RT_FLAG_TIME_KERNEL) {
@@ -1025,6 +1128,8 @@ rt_status rt_trace_rays(rt_context* ctx, const rt_scene* sc, const rt_render_opt
         RT_HIP(launch_trace_rays(p, path, true, d_rays, n, d_out, ctx->stream));
         unsigned long long c[2] = {0, 0};
         RT_HIP(hipMemcpyAsync(c, p.counters, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
+        st = scratch_done(ctx);  // the counters' last user is this read-back
+        if (st != RT_OK) return st;
         RT_HIP(hipStreamSynchronize(ctx->stream));
         stats->trace_rays = c[0];
         stats->shadow_rays = c[1];

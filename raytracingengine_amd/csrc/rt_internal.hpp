@@ -146,9 +146,15 @@ hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specu
                                 hipStream_t stream);
 size_t packet_lds_bytes(int ns, int np, int nl);
 hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t stream);
-// every frame of p.fr[0 .. nframes): its image at img + f * stride (doubles)
-hipError_t launch_packet_image_batch(const TraceParams& p, int nframes, double* img,
-                                     size_t stride, hipStream_t stream);
+// The images a frame batch forms before its launch: job j forms frame frame[j]'s image
+// (camera p.fr[frame[j]].cam) at dst[j] — a cache entry of the scene or a slot of its ring.
+struct PkImageJobs {
+    double* dst[kPkMaxBatch];
+    int32_t frame[kPkMaxBatch];
+    int32_t n;
+};
+hipError_t launch_packet_image_batch(const TraceParams& p, const PkImageJobs& jobs,
+                                     hipStream_t stream);
 // The packet kernel's launch shape for p (grid of workgroups, waves per workgroup), and the
 // costliest-first tile order built from the wave durations a launch of that shape recorded.
 void packet_grid(const TraceParams& p, uint32_t& gx, uint32_t& gy, uint32_t& waves);

@@ -9,10 +9,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rt_capi.h"
@@ -33,6 +35,13 @@ struct rt_comm {
     rt_context* ctx = nullptr;  // the context whose device and stream the renders use
     int device = -1;
     ncclComm_t nccl = nullptr;
+    // rt_comm_create: a non-blocking RCCL communicator whose calls wait with a deadline
+    // (comm_wait); past it, or on an asynchronous RCCL error, the communicator is aborted
+    // (ncclCommAbort) and every later call on it fails with RT_ERR_RCCL
+    bool nonblocking = false;
+    bool aborted = false;
+    long timeout_ms = 0;  // 0: no deadline
+    rtamd::DeviceBuffer chk;  // rt_comm_set_root_weight's agreement check (2 ints)
     // rt_comm_create_local: no RCCL communicator; rt_render_gather_all copies every rank's rows
     // into rank 0's receive buffer (`peers` = the group in rank order, on every member)
     bool local = false;
@@ -78,11 +87,60 @@ rt_status nccl_fail(ncclResult_t r, const char* what) {
     return fail(RT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-#define RT_NCCL(call)                                       \
-    do {                                                    \
-        ncclResult_t r_ = (call);                           \
-        if (r_ != ncclSuccess) return nccl_fail(r_, #call); \
+// ncclInProgress is how a non-blocking communicator's call returns: not an error (comm_wait
+// then waits for it).
+#define RT_NCCL(call)                                                                \
+    do {                                                                             \
+        ncclResult_t r_ = (call);                                                    \
+        if (r_ != ncclSuccess && r_ != ncclInProgress) return nccl_fail(r_, #call);  \
     } while (0)
+
+// Deadline of a communicator's waits (rt_comm_create; RTAMD_COMM_TIMEOUT_MS overrides; 0 = none).
+long default_comm_timeout_ms() {
+    const char* e = std::getenv("RTAMD_COMM_TIMEOUT_MS");
+    return e ? std::atol(e) : 300000L;
+}
+
+using Clock = std::chrono::steady_clock;
+
+bool past(const Clock::time_point& t0, long timeout_ms) {
+    return timeout_ms > 0 &&
+           std::chrono::duration_cast<std::chrono::milliseconds>(Clock::now() - t0).count() >=
+               timeout_ms;
+}
+
+// Aborts the communicator (its RCCL kernels in flight observe the abort and return) and fails.
+rt_status comm_abort(rt_comm* c, const std::string& what, const std::string& why) {
+    if (c->nccl) (void)ncclCommAbort(c->nccl);
+    c->nccl = nullptr;
+    c->aborted = true;
+    return fail(RT_ERR_RCCL, what + ": " + why + " (communicator aborted)");
+}
+
+rt_status comm_usable(const rt_comm* c, const char* what) {
+    if (c->aborted)
+        return fail(RT_ERR_RCCL, std::string(what) + ": the communicator was aborted earlier");
+    return RT_OK;
+}
+
+// Waits until the communicator's last RCCL call has been issued (ncclCommGetAsyncError leaves
+// ncclInProgress); an asynchronous error or the deadline aborts it.  Blocking communicators
+// (ncclCommInitAll) return at once unless an error is pending.
+rt_status comm_wait(rt_comm* c, const char* what) {
+    if (!c->nccl) return comm_usable(c, what);
+    const Clock::time_point t0 = Clock::now();
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = ncclCommGetAsyncError(c->nccl, &st);
+        if (r != ncclSuccess) st = r;
+        if (st == ncclSuccess) return RT_OK;
+        if (st != ncclInProgress) return comm_abort(c, what, ncclGetErrorString(st));
+        if (past(t0, c->timeout_ms))
+            return comm_abort(c, what, "no completion within " + std::to_string(c->timeout_ms) +
+                                           " ms");
+        std::this_thread::yield();
+    }
+}
 
 // This rank's share of the frame: rt_render_opts selecting the block-cyclic row set `rank` of
 // `n` (a contiguous full frame when n == 1), and the rows it produces.
@@ -292,6 +350,10 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cams, int
     }
     st = record(f.ev, 1, ctx->stream);
     if (st != RT_OK) return st;
+    // the render is the first thing rt_comm_destroy must wait for (it writes the send / receive
+    // buffers): recorded now, so a gather or assembly that fails to enqueue leaves it covered
+    RT_HIP(hipEventRecord(c->done, ctx->stream));
+    c->any_frame = true;
     if (f.pipelined) {
         RT_HIP(hipEventRecord(c->rendered[f.slot], ctx->stream));
         RT_HIP(hipStreamWaitEvent(f.gs, c->rendered[f.slot], 0));
@@ -677,9 +739,15 @@ rt_status rt_comm_unique_id(uint8_t* id) {
 
 rt_status rt_comm_create(rt_context* ctx, int nranks, int rank, const uint8_t* id,
                          rt_comm** out) {
+    return rt_comm_create_ex(ctx, nranks, rank, id, default_comm_timeout_ms(), out);
+}
+
+rt_status rt_comm_create_ex(rt_context* ctx, int nranks, int rank, const uint8_t* id,
+                            long timeout_ms, rt_comm** out) {
     if (!ctx || !id || !out) return fail(RT_ERR_INVALID_ARG, "NULL argument to rt_comm_create");
     if (nranks < 1 || rank < 0 || rank >= nranks)
         return fail(RT_ERR_INVALID_ARG, "rank must be in [0, nranks)");
+    if (timeout_ms < 0) return fail(RT_ERR_INVALID_ARG, "timeout_ms must be >= 0");
     *out = nullptr;
     DeviceGuard g(ctx->device);
     rt_comm* c = new (std::nothrow) rt_comm();
@@ -688,6 +756,7 @@ rt_status rt_comm_create(rt_context* ctx, int nranks, int rank, const uint8_t* i
     c->device = ctx->device;
     c->nranks = nranks;
     c->rank = rank;
+    c->timeout_ms = timeout_ms;
     rt_status st = init_streams(c);
     if (st != RT_OK) {
         rt_comm_destroy(c);
@@ -695,12 +764,32 @@ rt_status rt_comm_create(rt_context* ctx, int nranks, int rank, const uint8_t* i
     }
     ncclUniqueId u;
     std::memcpy(u.internal, id, sizeof u.internal);
-    const ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, u, rank);
-    if (r != ncclSuccess) {
+    // Non-blocking initialisation: a rank that never joins (a dead or missing peer process)
+    // makes the init time out here instead of blocking this rank forever.
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const ncclResult_t r = ncclCommInitRankConfig(&c->nccl, nranks, u, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+        if (c->nccl) (void)ncclCommAbort(c->nccl);
+        c->nccl = nullptr;
         rt_comm_destroy(c);
-        return nccl_fail(r, "ncclCommInitRank");
+        return nccl_fail(r, "ncclCommInitRankConfig");
+    }
+    c->nonblocking = true;
+    st = comm_wait(c, "ncclCommInitRankConfig");
+    if (st != RT_OK) {
+        const std::string msg = rt_last_error();
+        rt_comm_destroy(c);
+        return fail(st, msg);
     }
     *out = c;
+    return RT_OK;
+}
+
+rt_status rt_comm_set_timeout(rt_comm* c, long timeout_ms) {
+    if (!c) return fail(RT_ERR_INVALID_ARG, "comm is NULL");
+    if (timeout_ms < 0) return fail(RT_ERR_INVALID_ARG, "timeout_ms must be >= 0");
+    c->timeout_ms = timeout_ms;
     return RT_OK;
 }
 
@@ -790,7 +879,15 @@ rt_status rt_comm_destroy(rt_comm* c) {
             if (c->slot_used[s]) (void)hipEventSynchronize(c->freed[s]);
         (void)hipEventSynchronize(c->done);
     }
+    if (c->nccl && c->nonblocking) {
+        // a non-blocking communicator is finalized (its outstanding operations flushed) before
+        // it is freed; one that does not finish within the deadline is aborted instead
+        const ncclResult_t r = ncclCommFinalize(c->nccl);
+        if (r != ncclSuccess && r != ncclInProgress) (void)comm_abort(c, "ncclCommFinalize", ncclGetErrorString(r));
+        else (void)comm_wait(c, "ncclCommFinalize");
+    }
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    c->chk.release();
     for (auto* v : {&c->pending, &c->spare})
         for (auto& ev : *v)
             for (auto& x : ev.e) (void)hipEventDestroy(x);
@@ -813,9 +910,31 @@ rt_status rt_comm_destroy(rt_comm* c) {
 rt_status rt_comm_synchronize(rt_comm* c) {
     if (!c) return fail(RT_ERR_INVALID_ARG, "comm is NULL");
     DeviceGuard g(c->device);
-    RT_HIP(hipStreamSynchronize(c->ctx->stream));
-    RT_HIP(hipStreamSynchronize(c->gstream));
-    return RT_OK;
+    if (c->local || c->nranks == 1 || c->timeout_ms == 0 || !c->nccl) {
+        RT_HIP(hipStreamSynchronize(c->ctx->stream));
+        RT_HIP(hipStreamSynchronize(c->gstream));
+        return comm_usable(c, "rt_comm_synchronize");
+    }
+    // Polls both streams and the communicator: a gather whose peer never arrives (a rank that
+    // died or diverged) ends in an asynchronous RCCL error or the deadline, and the abort makes
+    // its kernels return instead of spinning on the GPU for ever.
+    const Clock::time_point t0 = Clock::now();
+    for (;;) {
+        const hipError_t a = hipStreamQuery(c->ctx->stream);
+        const hipError_t b = hipStreamQuery(c->gstream);
+        if (a == hipSuccess && b == hipSuccess) return RT_OK;
+        if (a != hipSuccess && a != hipErrorNotReady) return hip_fail(a, "hipStreamQuery");
+        if (b != hipSuccess && b != hipErrorNotReady) return hip_fail(b, "hipStreamQuery");
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = ncclCommGetAsyncError(c->nccl, &st);
+        if (r != ncclSuccess) st = r;
+        if (st != ncclSuccess && st != ncclInProgress)
+            return comm_abort(c, "rt_comm_synchronize", ncclGetErrorString(st));
+        if (past(t0, c->timeout_ms))
+            return comm_abort(c, "rt_comm_synchronize",
+                              "frames not finished within " + std::to_string(c->timeout_ms) + " ms");
+        std::this_thread::yield();
+    }
 }
 
 rt_status rt_render_gather(rt_comm* c, const rt_scene* sc, const rt_camera* cam,
@@ -843,6 +962,8 @@ rt_status rt_render_gather_batch(rt_comm* c, const rt_scene* sc, const rt_camera
     if (c->local && c->nranks > 1)
         return fail(RT_ERR_INVALID_ARG, "local communicators (rt_comm_create_local) gather "
                                         "through rt_render_gather_all");
+    st = comm_usable(c, "rt_render_gather_batch");
+    if (st != RT_OK) return st;
     DeviceGuard g(c->device);
     Frame f;
     st = render_part(c, sc, cams, nframes, opts, outputs, dst, local, f);
@@ -851,6 +972,8 @@ rt_status rt_render_gather_batch(rt_comm* c, const rt_scene* sc, const rt_camera
         RT_NCCL(ncclGroupStart());
         st = gather_part(c, cams, outputs, f);
         RT_NCCL(ncclGroupEnd());
+        if (st != RT_OK) return st;
+        st = comm_wait(c, "ncclGather");
         if (st != RT_OK) return st;
     }
     return assemble_part(c, cams, outputs, f, dst);
@@ -878,6 +1001,17 @@ rt_status rt_render_gather_all_batch(rt_comm* const* comms, rt_scene* const* sce
             return fail(RT_ERR_INVALID_ARG, "rt_render_gather_all: comms must be the n ranks of "
                                             "one rt_comm_create_all / rt_comm_create_local, in "
                                             "rank order");
+    for (int i = 0; i < n; ++i) {
+        // every rank sizes its send buffer and rank 0 its receive slots from the same split
+        if (comms[i]->root_weight != comms[0]->root_weight)
+            return fail(RT_ERR_INVALID_ARG, "rt_render_gather_all: rank " + std::to_string(i) +
+                                                " has root weight " +
+                                                std::to_string(comms[i]->root_weight) +
+                                                ", rank 0 " +
+                                                std::to_string(comms[0]->root_weight));
+        st = comm_usable(comms[i], "rt_render_gather_all");
+        if (st != RT_OK) return st;
+    }
     void* const dst[3] = {d_hdr64, d_hdr32, d_ldr};
     st = check_root_outputs(comms[0], outputs, dst);
     if (st != RT_OK) return st;
@@ -897,6 +1031,8 @@ rt_status rt_render_gather_all_batch(rt_comm* const* comms, rt_scene* const* sce
             st = gather_part(comms[i], cams, outputs, f[i]);
         }
         RT_NCCL(ncclGroupEnd());
+        if (st != RT_OK) return st;
+        for (int i = 0; i < n && st == RT_OK; ++i) st = comm_wait(comms[i], "ncclGather");
         if (st != RT_OK) return st;
     }
     for (int i = 0; i < n; ++i) {  // 3. rank 0 assembles; the others close their events
@@ -952,11 +1088,34 @@ rt_status rt_comm_set_root_weight(rt_comm* c, int weight) {
         return fail(RT_ERR_INVALID_ARG, "root weight must be in [1, 64]");
     if (weight > 1 && c->nranks + weight - 1 > 65535)
         return fail(RT_ERR_INVALID_ARG, "too many row sets");
+    rt_status st = comm_usable(c, "rt_comm_set_root_weight");
+    if (st != RT_OK) return st;
+    DeviceGuard g(c->device);
     if (c->any_frame && weight != c->root_weight) {
         // frames in flight were planned with the old weight: wait for them
-        DeviceGuard g(c->device);
-        RT_HIP(hipStreamSynchronize(c->ctx->stream));
-        RT_HIP(hipStreamSynchronize(c->gstream));
+        st = rt_comm_synchronize(c);
+        if (st != RT_OK) return st;
+    }
+    if (c->nccl && c->nranks > 1) {
+        // Collective on a communicator of one process per GPU: every rank must plan the same
+        // split (a peer sizing its send from another weight than rank 0's receive would read
+        // past buffers or pair ncclSend with ncclGather and hang), so the ranks agree on it
+        // first — one all-reduce (max of {w, -w}) — and every rank fails alike if they differ.
+        RT_HIP(c->chk.ensure(2 * sizeof(int32_t)));
+        const int32_t v[2] = {weight, -weight};
+        RT_HIP(hipMemcpyAsync(c->chk.ptr, v, sizeof v, hipMemcpyHostToDevice, c->ctx->stream));
+        RT_NCCL(ncclAllReduce(c->chk.ptr, c->chk.ptr, 2, ncclInt32, ncclMax, c->nccl,
+                              c->ctx->stream));
+        st = comm_wait(c, "ncclAllReduce");
+        if (st != RT_OK) return st;
+        int32_t m[2] = {0, 0};
+        RT_HIP(hipMemcpyAsync(m, c->chk.ptr, sizeof m, hipMemcpyDeviceToHost, c->ctx->stream));
+        st = rt_comm_synchronize(c);
+        if (st != RT_OK) return st;
+        if (m[0] != weight || -m[1] != weight)
+            return fail(RT_ERR_INVALID_ARG, "rt_comm_set_root_weight: the ranks asked for "
+                                            "different weights (" + std::to_string(-m[1]) + ".." +
+                                            std::to_string(m[0]) + "); the weight is unchanged");
     }
     c->root_weight = weight;
     return RT_OK;

@@ -1445,19 +1445,23 @@ hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t st
     return hipGetLastError();
 }
 
-// The images of a frame batch's cameras, one workgroup per frame (pk_build_image: the same
-// words a workgroup of the batch launch would form for itself).
-__global__ __launch_bounds__(256) void packet_image_batch_kernel(TraceParams P, double* img,
-                                                                 size_t stride) {
-    pk_build_image(P, P.fr[blockIdx.x].cam, img + blockIdx.x * stride,
-                   static_cast<int>(threadIdx.x), 256);
+// The images of a frame batch's uncached cameras, one workgroup per job (pk_build_image: the
+// same words a workgroup of the batch launch would form for itself), each written where the
+// host put it: a new cache entry (a camera seen before) or the batch's ring slot.
+__global__ __launch_bounds__(256) void packet_image_batch_kernel(TraceParams P, PkImageJobs J) {
+    const int f = J.frame[blockIdx.x];
+    pk_build_image(P, P.fr[f].cam, J.dst[blockIdx.x], static_cast<int>(threadIdx.x), 256);
 }
 
-hipError_t launch_packet_image_batch(const TraceParams& p, int nframes, double* img,
-                                     size_t stride, hipStream_t stream) {
-    if (nframes <= 0) return hipSuccess;
-    hipLaunchKernelGGL(packet_image_batch_kernel, dim3(static_cast<unsigned>(nframes)),
-                       dim3(256), 0, stream, p, img, stride);
+hipError_t launch_packet_image_batch(const TraceParams& p, const PkImageJobs& jobs,
+                                     hipStream_t stream) {
+    if (jobs.n <= 0) return hipSuccess;
+    if (jobs.n > kPkMaxBatch) return hipErrorInvalidValue;
+    for (int j = 0; j < jobs.n; ++j)
+        if (!jobs.dst[j] || jobs.frame[j] < 0 || jobs.frame[j] >= static_cast<int>(p.nframes))
+            return hipErrorInvalidValue;
+    hipLaunchKernelGGL(packet_image_batch_kernel, dim3(static_cast<unsigned>(jobs.n)),
+                       dim3(256), 0, stream, p, jobs);
     return hipGetLastError();
 }
 

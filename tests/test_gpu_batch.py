@@ -365,3 +365,110 @@ def test_moving_batches_on_two_streams_reuse_the_image_ring(ctx):
         ctx.set_stream(None)
         ds.camera["position"][0] = base
         ds.close()
+
+
+# ------------------------------------------------------------------ the bench's launch shapes
+@pytest.mark.parametrize("nf", [32, 20])
+def test_batch_full_c2_bench_launch_shape_is_the_reference(ctx, golden, nf):
+    """The bench's own launch at full size: ONE 1920x1080 C2 launch of 32 static-camera frames
+    (the default batch) and of 20 (the driver's `--steps 20` timed region): every frame's HDR and
+    Reinhard bytes have the reference's SHA-256, on the fresh-camera, cache-creating and cached
+    launches (RE/Scene.h:311-328)."""
+    info = golden["meta"]["scenes"]["c2_full"]
+    sc = make_config("c2")
+    ds = ctx.scene(sc)
+    W, H = sc.camera.width, sc.camera.height
+    try:
+        cams = ds.cameras(np.repeat(ds.camera["position"], nf, axis=0))
+        H64 = torch.empty(nf * H * W * 3, dtype=torch.float64, device="cuda")
+        L8 = torch.empty(nf * H * W * 3, dtype=torch.uint8, device="cuda")
+        for rnd in range(3):
+            H64.fill_(-1.0)
+            L8.zero_()
+            torch.cuda.synchronize()
+            ds.render_batch(cams, H64.data_ptr(), None, L8.data_ptr(), capi.default_opts(tonemap=1))
+            ctx.synchronize()
+            a64 = H64.cpu().numpy().reshape(nf, -1)
+            a8 = L8.cpu().numpy().reshape(nf, -1)
+            for f in range(nf):
+                assert _sha(a64[f]) == info["image_sha256"], (rnd, f)
+                assert _sha(a8[f]) == info["ldr_sha256"]["reinhard_simple"], (rnd, f)
+    finally:
+        ds.close()
+
+
+def test_batch_full_c2_moving_camera_revisits_vs_oracle(ctx, oracle):
+    """A 1920x1080 C2 batch of 32 frames whose camera moves every frame and revisits 5 positions
+    an earlier batch rendered (second sightings: their images become cache entries inside the
+    batch's one image launch, no launch of their own), plus a frame repeated inside the batch.
+    Every frame equals the C oracle rendering its camera, bit for bit (HDR), and the Reinhard
+    bytes equal the oracle's tonemap; a second pass (every image cached now) gives the same."""
+    sc = make_config("c2")
+    ds = ctx.scene(sc)
+    W, H = sc.camera.width, sc.camera.height
+    base = np.array(sc.camera.position)
+    try:
+        early = [base + (0.013 * (i + 1), -0.007 * i, 0.011 * i) for i in range(5)]
+        warm = torch.empty(5 * H * W * 3, dtype=torch.uint8, device="cuda")
+        ds.render_batch(ds.cameras(np.array(early)), None, None, warm.data_ptr(),
+                        capi.default_opts(tonemap=1))
+        ctx.synchronize()
+        fresh = [base + (-0.02 * (i + 1), 0.004 * i, -0.009 * i) for i in range(26)]
+        pos = np.array(early + fresh[:13] + [fresh[3]] + fresh[13:])  # frame 18 repeats 8
+        assert len(pos) == 32
+        H64 = torch.empty(32 * H * W * 3, dtype=torch.float64, device="cuda")
+        L8 = torch.empty(32 * H * W * 3, dtype=torch.uint8, device="cuda")
+        got = []
+        for rnd in range(2):
+            H64.fill_(-1.0)
+            L8.zero_()
+            torch.cuda.synchronize()
+            ds.render_batch(ds.cameras(pos), H64.data_ptr(), None, L8.data_ptr(),
+                            capi.default_opts(tonemap=1))
+            ctx.synchronize()
+            got.append((H64.cpu().numpy().reshape(32, H, W, 3), L8.cpu().numpy().reshape(32, -1)))
+    finally:
+        ds.close()
+    for f in range(32):
+        scf = dataclasses.replace(sc, camera=dataclasses.replace(sc.camera,
+                                                                 position=tuple(pos[f])))
+        ref, _, _ = oracle.render(scf)
+        ref8 = oracle.tonemap(ref, 1).reshape(-1)
+        for rnd in range(2):
+            assert np.array_equal(got[rnd][0][f], ref), (rnd, f)
+            assert np.array_equal(got[rnd][1][f], ref8), (rnd, f)
+
+
+def test_gather_all_batch_rejects_unequal_root_weights():
+    """Every rank must plan the same split: a weight set on rank 0 only (or on the peers only)
+    is an invalid argument, never a copy past a peer's send buffer."""
+    ctxs = [capi.Context(0) for _ in range(3)]
+    try:
+        comms = capi.Comm.create_local(ctxs)
+        sc = make_config("c2", 160, 90)
+        scenes = [c.scene(sc) for c in ctxs]
+        L8 = torch.zeros(90 * 160 * 3, dtype=torch.uint8, device="cuda")
+        opts = capi.default_opts(tonemap=1, row_block=16)
+        for who in ([0], [1, 2]):
+            for i in who:
+                comms[i].set_root_weight(3)
+            with pytest.raises(capi.RtError) as e:
+                capi.render_gather_all_batch(comms, scenes, scenes[0].cameras(
+                    scenes[0].camera["position"]), opts, capi.RT_OUT_LDR, d_ldr=L8.data_ptr())
+            assert e.value.status == capi.RT_ERR_INVALID_ARG
+            assert "root weight" in str(e.value)
+            for c in comms:
+                c.set_root_weight(1)
+        capi.render_gather_all_batch(comms, scenes, scenes[0].cameras(
+            scenes[0].camera["position"]), opts, capi.RT_OUT_LDR, d_ldr=L8.data_ptr())
+        for c in comms:
+            c.synchronize()
+        ref = scenes[0].render(tonemap=1)["ldr"]
+        assert np.array_equal(L8.cpu().numpy().reshape(90, 160, 3), ref)
+        for s in scenes:
+            s.close()
+        for c in comms:
+            c.close()
+    finally:
+        for c in ctxs:
+            c.close()

@@ -318,3 +318,75 @@ def test_render_multi_shared_device_group_lifetime():
     finally:
         for c in cs:
             c.close()                       # root first this time, then the members
+
+
+# ------------------------------------------------------------------ failure detection
+_MISSING_PEER = r'''
+import json, sys, time, hashlib
+import numpy as np
+from raytracingengine_amd import capi
+from raytracingengine_amd.configs import make_config
+ctx = capi.Context(0)
+t0 = time.perf_counter()
+status, msg = 0, ""
+try:
+    c = capi.Comm(ctx, 2, 0, capi.comm_unique_id(), timeout_ms=int(sys.argv[1]))
+    c.close()
+except capi.RtError as e:
+    status, msg = e.status, str(e)
+dt = time.perf_counter() - t0
+sc = make_config("c2", 192, 108)
+ds = ctx.scene(sc)
+out = ds.render(hdr64=True, tonemap=1)
+ds.close()
+print(json.dumps({"status": status, "msg": msg, "seconds": dt,
+                  "sha": hashlib.sha256(out["hdr64"].tobytes()).hexdigest()}))
+'''
+
+
+def test_comm_missing_peer_fails_within_deadline_then_renders(oracle):
+    """Rank 0 of a 2-rank communicator whose peer never joins: the non-blocking
+    ncclCommInitRankConfig polled with a 3 s deadline returns RT_ERR_RCCL (communicator aborted)
+    instead of blocking, and the same process then renders a frame equal to the oracle's.  Run
+    in a child process under its own time limit, so a regression cannot hang the suite."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    p = subprocess.run([sys.executable, "-c", _MISSING_PEER, "3000"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=100)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["status"] == capi.RT_ERR_RCCL, r
+    assert "aborted" in r["msg"], r
+    assert 2.5 <= r["seconds"] < 30.0, r
+    sc = make_config("c2", 192, 108)
+    ref, _, _ = oracle.render(sc)
+    assert r["sha"] == _sha(ref)
+
+
+def test_comm_with_deadline_renders_and_synchronizes(ctx):
+    """A 1-rank communicator through rt_comm_create_ex (non-blocking init, 10 s deadline) and a
+    changed deadline: frames render and synchronize as with rt_comm_create; a negative deadline
+    is an invalid argument."""
+    c = capi.Comm(ctx, 1, 0, capi.comm_unique_id(), timeout_ms=10000)
+    try:
+        c.set_timeout(5000)
+        sc = make_config("c2", 160, 90)
+        ds = ctx.scene(sc)
+        try:
+            ref = ds.render(tonemap=1)["ldr"]
+            d8 = torch.zeros(90 * 160 * 3, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            c.render_gather(ds, capi.default_opts(tonemap=1), capi.RT_OUT_LDR, d_ldr=d8.data_ptr())
+            c.synchronize()
+            assert np.array_equal(d8.cpu().numpy().reshape(90, 160, 3), ref)
+        finally:
+            ds.close()
+        with pytest.raises(capi.RtError) as e:
+            c.set_timeout(-1)
+        assert e.value.status == capi.RT_ERR_INVALID_ARG
+    finally:
+        c.close()
