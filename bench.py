@@ -74,8 +74,12 @@ def parse_args(argv=None):
     ap.add_argument("--clock-warmup-ms", type=float, default=50.0,
                     help="untimed frames for this much wall time before the W warmup frames, so "
                          "that the K timed frames run at the GPU's sustained clock")
-    ap.add_argument("--event-every", type=int, default=4,
-                    help="bracket every n-th timed batch with HIP events (0: none)")
+    ap.add_argument("--event-every", type=int, default=None,
+                    help="bracket every n-th timed batch with per-batch HIP events (render / "
+                         "gather / assembly per rank); 0: none — the kernel time then comes from "
+                         "the HIP events on the launch stream around the whole timed region.  "
+                         "Default: 0 at N=1 (in-region event records cost ~30 us of a 20-frame "
+                         "region, tools/host_overhead.py), 4 at N>1")
     ap.add_argument("--no-extras", action="store_true",
                     help="headline only (no extra fields)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -402,8 +406,9 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
                                 ldr[0].data_ptr() if root else local[1].data_ptr(), wopts)
 
     comm.timing(reset=True)
-    elapsed, _ = R.timed(step, frames, warmup, batch, warm_step=warm_step if split else None,
-                         sync=comm.synchronize if split else None)
+    elapsed, region_ms = R.timed(step, frames, warmup, batch,
+                                 warm_step=warm_step if split else None,
+                                 region_events=True, sync=comm.synchronize if split else None)
     t = comm.timing(reset=True)
     if split and weight != 1:
         comm.set_root_weight(1)
@@ -416,7 +421,15 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     return {"elapsed": elapsed, "rays": rays_all, "rays_rank": rays_rank, "ranks": ranks,
             "px": W * H, "rows": rows, "frames": frames, "batch": batch,
             "gather_bytes_per_frame": max_rows * W * 3 if split else 0, "root_weight": weight,
-            "bufs": (local, ldr)}
+            "region_ms": region_ms, "launches": -(-frames // batch), "bufs": (local, ldr)}
+
+
+def kernel_ms_per_frame(res, event_every):
+    """Rank 0's render time per frame: per-batch HIP events (event_every > 0) or the HIP events
+    on the launch stream around the whole timed region."""
+    if event_every > 0:
+        return res["ranks"][0][0]
+    return res["region_ms"] / max(res["frames"], 1)
 
 
 def per_rank_summary(res):
@@ -505,6 +518,8 @@ def workload_text(sc, world, block, batch, hdr, tonemap_name):
 def main(argv=None):
     args = parse_args(argv)
     R = Runner(args)
+    if args.event_every is None:
+        args.event_every = 0 if R.world == 1 else 4
     capi = R.capi
     from raytracingengine_amd.configs import make_config
 
@@ -534,11 +549,24 @@ def main(argv=None):
     value = res["rays"] * args.steps / elapsed / 1e6
     summ = per_rank_summary(res)
     r0 = res["ranks"][0]
-    # the trace kernel: rank 0's render per frame (HIP events around each timed batch launch)
-    render_ms = r0[0]
-    ev_launches = max(int(r0[6]), 1)
-    frames_per_launch = r0[5] / ev_launches      # the frames the event-timed launches held
-    launch_ms = r0[7] / ev_launches               # measured per launch, not render_ms x batch
+    # the trace kernel: rank 0's render per frame — from HIP events around every
+    # event_every-th timed batch launch, or (event_every 0, the N=1 default) from the HIP events
+    # on the launch stream around the whole timed region (launch gaps included)
+    if args.event_every > 0:
+        render_ms = r0[0]
+        ev_launches = max(int(r0[6]), 1)
+        frames_per_launch = r0[5] / ev_launches   # the frames the event-timed launches held
+        launch_ms = r0[7] / ev_launches           # measured per launch, not render_ms x batch
+        timing_src = (f"HIP events around every {args.event_every}-th timed batch launch on the "
+                      f"launch stream; those launches held {frames_per_launch:g} frames each")
+    else:
+        render_ms = res["region_ms"] / args.steps
+        frames_per_launch = args.steps / res["launches"]
+        launch_ms = res["region_ms"] / res["launches"]
+        timing_src = (f"HIP events on the launch stream around the whole timed region "
+                      f"({res['launches']} launch(es) of up to {batch} frames, "
+                      f"{frames_per_launch:g} frames per launch on average; gaps between "
+                      f"launches included)")
     bytes_per_frame = int(r0[3]) * W * (HDR_BYTES[args.hdr] + 3)
     achieved = bytes_per_frame / (render_ms / 1e3) / 1e9 if render_ms > 0 else 0.0
     # §8(d)'s FLOP roofline: F_ray = 25·Ns + 14·Np FP64 flops per ray of the reference's
@@ -600,9 +628,7 @@ def main(argv=None):
                            f"/ {FP64_VALU_PEAK_TF} TF; culling skips most of that work, so this "
                            "is the reference algorithm's rate, not counted flops (valu)"),
             "note": "rank 0's batch launch: its rows' framebuffer bytes (HDR + u8) per frame / "
-                    "its render time per frame (HIP events around every "
-                    f"{args.event_every}-th timed batch launch; those launches held "
-                    f"{frames_per_launch:g} frames each)",
+                    f"its render time per frame ({timing_src})",
         },
         "valu": valu if R.world == 1 else None,
         "valu_source": valu_src if R.world == 1 else None,
@@ -618,7 +644,8 @@ def main(argv=None):
                                  "note": "every rank its own whole frames, one launch each "
                                          "(rt_render_device)"}
         # weak scaling: every rank its own whole frames, batched
-        wk = split_frames(R, sc, steps_x, args.warmup, batch, args.hdr, tonemap, gather=False)
+        wk = split_frames(R, sc, steps_x, args.warmup, batch, args.hdr, tonemap, gather=False,
+                          event_every=args.event_every)
         (rays_w,) = R.sum_over_ranks(float(wk["rays_rank"]))
         line["weak_frames"] = {
             "value": round(rays_w * steps_x / wk["elapsed"] / 1e6, 3),
@@ -626,8 +653,9 @@ def main(argv=None):
             "workload": f"{sc.name} whole frames on every rank ({args.hdr} HDR + u8), "
                         f"{batch} per call"}
         if R.world == 1:
-            f32 = split_frames(R, sc, steps_x, args.warmup, batch, "f32", tonemap)
-            k32 = f32["ranks"][0][0]
+            f32 = split_frames(R, sc, steps_x, args.warmup, batch, "f32", tonemap,
+                               event_every=args.event_every)
+            k32 = kernel_ms_per_frame(f32, args.event_every)
             b32 = res["px"] * 15
             a32 = b32 / (k32 / 1e3) / 1e9 if k32 > 0 else 0.0
             line["roofline_f32"] = {
@@ -636,10 +664,11 @@ def main(argv=None):
                 "kernel_ms_per_frame": round(k32, 6),
                 "value": round(f32["rays"] * steps_x / f32["elapsed"] / 1e6, 3)}
             mv = split_frames(R, sc, steps_x, args.warmup, batch, args.hdr, tonemap,
+                              event_every=args.event_every,
                               camera_step=lambda base, i: base + (i * 1e-7, 0.0, 0.0))
             line["moving_camera"] = {
                 "ms_per_step": round(mv["elapsed"] / steps_x * 1e3, 5),
-                "kernel_ms_per_frame": round(mv["ranks"][0][0], 6),
+                "kernel_ms_per_frame": round(kernel_ms_per_frame(mv, args.event_every), 6),
                 "value": round(mv["rays"] * steps_x / mv["elapsed"] / 1e6, 3),
                 "note": "camera x moved by 1e-7 every frame: no frame reuses a cached per-camera "
                         "packet image (one small launch per batch forms every frame's image "

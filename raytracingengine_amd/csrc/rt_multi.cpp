@@ -69,6 +69,7 @@ struct rt_comm {
     struct Ev {
         hipEvent_t e[5];
         int frames = 1;  // frames of the batch these events bracket
+        bool direct = false;  // one rank: only the render's two events are recorded
     };
     std::vector<Ev> pending, spare;
     double render_ms = 0, gather_ms = 0, assemble_ms = 0;
@@ -214,12 +215,15 @@ rt_status check_outputs(int outputs) {
 rt_status harvest(rt_comm* c, bool all) {
     size_t done = 0;
     for (auto& ev : c->pending) {
-        if (!all && hipEventQuery(ev.e[4]) != hipSuccess) break;
-        RT_HIP(hipEventSynchronize(ev.e[4]));
+        const hipEvent_t last = ev.direct ? ev.e[1] : ev.e[4];
+        if (!all && hipEventQuery(last) != hipSuccess) break;
+        RT_HIP(hipEventSynchronize(last));
         float a = 0, b = 0, d = 0;
         RT_HIP(hipEventElapsedTime(&a, ev.e[0], ev.e[1]));
-        RT_HIP(hipEventElapsedTime(&b, ev.e[2], ev.e[3]));
-        RT_HIP(hipEventElapsedTime(&d, ev.e[3], ev.e[4]));
+        if (!ev.direct) {
+            RT_HIP(hipEventElapsedTime(&b, ev.e[2], ev.e[3]));
+            RT_HIP(hipEventElapsedTime(&d, ev.e[3], ev.e[4]));
+        }
         c->render_ms += a;
         c->gather_ms += b;
         c->assemble_ms += d;
@@ -303,6 +307,7 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cams, int
             for (auto& x : e.e) RT_HIP(hipEventCreate(&x));
         }
         e.frames = nframes;
+        e.direct = f.direct;
         f.ev = &e;
     }
     // the frame's own events replace the per-launch ones of the render
@@ -350,15 +355,20 @@ rt_status render_part(rt_comm* c, const rt_scene* sc, const rt_camera* cams, int
     }
     st = record(f.ev, 1, ctx->stream);
     if (st != RT_OK) return st;
-    // the render is the first thing rt_comm_destroy must wait for (it writes the send / receive
-    // buffers): recorded now, so a gather or assembly that fails to enqueue leaves it covered
-    RT_HIP(hipEventRecord(c->done, ctx->stream));
-    c->any_frame = true;
     if (f.pipelined) {
         RT_HIP(hipEventRecord(c->rendered[f.slot], ctx->stream));
         RT_HIP(hipStreamWaitEvent(f.gs, c->rendered[f.slot], 0));
     }
-    return record(f.ev, 2, f.gs);
+    return f.direct ? RT_OK : record(f.ev, 2, f.gs);
+}
+
+// A batch whose render was enqueued but whose gather or assembly then failed: rt_comm_destroy
+// must still wait for the render (it writes the send / receive buffers) — its `done` event is
+// recorded behind it here, since assemble_part never ran.
+rt_status after_failed_frame(rt_comm* c, rt_status st) {
+    if (c->ctx && c->ctx->stream && hipEventRecord(c->done, c->ctx->stream) == hipSuccess)
+        c->any_frame = true;
+    return st;
 }
 
 // Phase 2: one ncclGather per output of the whole batch (inside the caller's group): the send
@@ -440,7 +450,7 @@ rt_status gather_local(rt_comm* const* comms, int n, const rt_camera* cam, int o
 // Phase 3 (rank 0): gathered rows into image order in the caller's device framebuffers.
 rt_status assemble_part(rt_comm* c, const rt_camera* cam, int outputs, const Frame& f,
                         void* const* dst) {
-    rt_status st = record(f.ev, 3, f.gs);
+    rt_status st = f.direct ? RT_OK : record(f.ev, 3, f.gs);
     if (st != RT_OK) return st;
     if (c->rank == 0 && !f.direct) {
         for (int k = 0; k < 3; ++k) {
@@ -451,7 +461,7 @@ rt_status assemble_part(rt_comm* c, const rt_camera* cam, int outputs, const Fra
                                         f.pl.max_rows, static_cast<uint32_t>(f.nframes), f.gs));
         }
     }
-    st = record(f.ev, 4, f.gs);
+    st = f.direct ? RT_OK : record(f.ev, 4, f.gs);
     if (st != RT_OK) return st;
     if (f.pipelined) {
         RT_HIP(hipEventRecord(c->freed[f.slot], f.gs));
@@ -969,14 +979,18 @@ rt_status rt_render_gather_batch(rt_comm* c, const rt_scene* sc, const rt_camera
     st = render_part(c, sc, cams, nframes, opts, outputs, dst, local, f);
     if (st != RT_OK) return st;
     if (!f.direct) {
-        RT_NCCL(ncclGroupStart());
+        const ncclResult_t r0 = ncclGroupStart();
+        if (r0 != ncclSuccess) return after_failed_frame(c, nccl_fail(r0, "ncclGroupStart"));
         st = gather_part(c, cams, outputs, f);
-        RT_NCCL(ncclGroupEnd());
-        if (st != RT_OK) return st;
+        const ncclResult_t r1 = ncclGroupEnd();
+        if (st != RT_OK) return after_failed_frame(c, st);
+        if (r1 != ncclSuccess && r1 != ncclInProgress)
+            return after_failed_frame(c, nccl_fail(r1, "ncclGroupEnd"));
         st = comm_wait(c, "ncclGather");
-        if (st != RT_OK) return st;
+        if (st != RT_OK) return after_failed_frame(c, st);
     }
-    return assemble_part(c, cams, outputs, f, dst);
+    st = assemble_part(c, cams, outputs, f, dst);
+    return st == RT_OK ? st : after_failed_frame(c, st);
 }
 
 rt_status rt_render_gather_all(rt_comm* const* comms, rt_scene* const* scenes, int n,
@@ -1016,29 +1030,40 @@ rt_status rt_render_gather_all_batch(rt_comm* const* comms, rt_scene* const* sce
     st = check_root_outputs(comms[0], outputs, dst);
     if (st != RT_OK) return st;
     std::vector<Frame> f(static_cast<size_t>(n));
+    int rendered = 0;  // ranks whose render is enqueued: on failure, destroy waits for them
+    auto failed = [&](rt_status e) {
+        for (int i = 0; i < rendered; ++i) {
+            DeviceGuard g(comms[i]->device);
+            (void)after_failed_frame(comms[i], e);
+        }
+        return e;
+    };
     for (int i = 0; i < n; ++i) {  // 1. every GPU renders its rows (asynchronous)
         DeviceGuard g(comms[i]->device);
         st = render_part(comms[i], scenes[i], cams, nframes, opts, outputs, dst, nullptr, f[i]);
-        if (st != RT_OK) return st;
+        if (st != RT_OK) return failed(st);
+        rendered = i + 1;
     }
     if (comms[0]->local) {  // 2. the gather as device copies into rank 0's receive buffer
         st = gather_local(comms, n, cams, outputs, f);
-        if (st != RT_OK) return st;
+        if (st != RT_OK) return failed(st);
     } else if (!f[0].direct) {  // 2. one gather per frame and output over all GPUs
-        RT_NCCL(ncclGroupStart());
+        const ncclResult_t r0 = ncclGroupStart();
+        if (r0 != ncclSuccess) return failed(nccl_fail(r0, "ncclGroupStart"));
         for (int i = 0; i < n && st == RT_OK; ++i) {
             DeviceGuard g(comms[i]->device);
             st = gather_part(comms[i], cams, outputs, f[i]);
         }
-        RT_NCCL(ncclGroupEnd());
-        if (st != RT_OK) return st;
+        const ncclResult_t r1 = ncclGroupEnd();
+        if (st != RT_OK) return failed(st);
+        if (r1 != ncclSuccess && r1 != ncclInProgress) return failed(nccl_fail(r1, "ncclGroupEnd"));
         for (int i = 0; i < n && st == RT_OK; ++i) st = comm_wait(comms[i], "ncclGather");
-        if (st != RT_OK) return st;
+        if (st != RT_OK) return failed(st);
     }
     for (int i = 0; i < n; ++i) {  // 3. rank 0 assembles; the others close their events
         DeviceGuard g(comms[i]->device);
         st = assemble_part(comms[i], cams, outputs, f[i], dst);
-        if (st != RT_OK) return st;
+        if (st != RT_OK) return failed(st);
     }
     return RT_OK;
 }

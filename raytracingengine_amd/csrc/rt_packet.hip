@@ -124,42 +124,7 @@ __device__ __forceinline__ int cull_lane() {
 #endif
 }
 
-// ------------------------------------------------------------------ wave reductions (FP32)
-// Every lane must be active.  Floats are reduced as order-preserving int32 keys (sign-magnitude
-// to two's complement), so each step is one integer min/max on a DPP-permuted operand: four
-// steps reduce each 16-lane row (quad xor-1, quad xor-2, half-mirror, mirror), then the four row
-// values are combined in SGPRs.  NaN keys sort above +inf (a max returns NaN, a min skips it).
-template <int CTRL>
-__device__ __forceinline__ int dpp(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
-}
-__device__ __forceinline__ int f2key(float v) {
-    const int b = __float_as_int(v);
-    return b ^ ((b >> 31) & 0x7fffffff);
-}
-__device__ __forceinline__ float key2f(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
-template <int OP>  // 0 min, 1 max
-__device__ __forceinline__ float wave_red(float x) {
-    auto op = [](int a, int b) { return OP == 0 ? (a < b ? a : b) : (a < b ? b : a); };
-    int v = f2key(x);
-    v = op(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
-    v = op(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
-    v = op(v, dpp<0x141>(v));  // row_half_mirror
-    v = op(v, dpp<0x140>(v));  // row_mirror
-    const int r = op(op(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
-                     op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
-    return key2f(r);
-}
-
-// Lane `l`'s double / vector, broadcast to every lane (exact: a bit copy via SGPRs).
-__device__ __forceinline__ double lane_d(double v, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ d3 lane_d3(d3 v, int l) {
-    return mk(lane_d(v.x, l), lane_d(v.y, l), lane_d(v.z, l));
-}
+// (wave reductions, lane broadcasts: rt_trace_common.hpp)
 
 // A sphere of the packet image (LDS): kPkSph doubles — cx cy cz r², the camera-cone terms as 8
 // floats (cone_terms: vx vy vz q | rr dv slack r, r = the culling radius rounded up), the
@@ -1055,8 +1020,17 @@ __device__ __forceinline__ void pk_build_image(const TraceParams& P, const doubl
 
 }
 
+// Waves per SIMD of a variant (its register budget).
+constexpr int pk_waves(int MAXC, int FEAT, bool COUNT, bool MULTI) {
+    return (FEAT == 0 && MAXC == 1 && !MULTI && !COUNT) ? RT_PACKET_SMALL_WAVES
+         : (FEAT == (kFeatArea | kFeatNoPL) && !MULTI && !COUNT) ? RT_PACKET_AREA_WAVES
+         : FEAT == kFeatTris ? RT_PACKET_TRIS_WAVES
+         : (((FEAT == 0 || (FEAT & ~kFeatNoPL) == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4)
+                ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES)
+                : 1);
+}
 template <int MAXC, int FEAT, bool COUNT, bool MULTI, int WGY>  // MULTI = false: one sample (AA = 1)
-__global__ __launch_bounds__(64 * kWgWavesX * WGY, (FEAT == 0 && MAXC == 1 && !MULTI && !COUNT) ? RT_PACKET_SMALL_WAVES : (FEAT == (kFeatArea | kFeatNoPL) && !MULTI && !COUNT) ? RT_PACKET_AREA_WAVES : FEAT == kFeatTris ? RT_PACKET_TRIS_WAVES : (((FEAT == 0 || (FEAT & ~kFeatNoPL) == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4) ? (MULTI ? (FEAT == 0 ? RT_PACKET_LEAN_WAVES : 1) : RT_PACKET_AA1_WAVES) : 1)) void packet_direct_kernel(TraceParams P) {
+__global__ __launch_bounds__(64 * kWgWavesX * WGY, pk_waves(MAXC, FEAT, COUNT, MULTI)) void packet_direct_kernel(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int tid = threadIdx.x;
     constexpr bool kNoPL = (FEAT & kFeatNoPL) != 0;  // the launcher checked P.np == P.nl == 0

@@ -14,6 +14,43 @@
 
 namespace rtamd {
 
+// ------------------------------------------------------------------ wave reductions (FP32)
+// Every lane must be active.  Floats are reduced as order-preserving int32 keys (sign-magnitude
+// to two's complement), so each step is one integer min/max on a DPP-permuted operand: four
+// steps reduce each 16-lane row (quad xor-1, quad xor-2, half-mirror, mirror), then the four row
+// values are combined in SGPRs.  NaN keys sort above +inf (a max returns NaN, a min skips it).
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int f2key(float v) {
+    const int b = __float_as_int(v);
+    return b ^ ((b >> 31) & 0x7fffffff);
+}
+__device__ __forceinline__ float key2f(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
+template <int OP>  // 0 min, 1 max
+__device__ __forceinline__ float wave_red(float x) {
+    auto op = [](int a, int b) { return OP == 0 ? (a < b ? a : b) : (a < b ? b : a); };
+    int v = f2key(x);
+    v = op(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = op(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = op(v, dpp<0x141>(v));  // row_half_mirror
+    v = op(v, dpp<0x140>(v));  // row_mirror
+    const int r = op(op(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+                     op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+    return key2f(r);
+}
+
+// Lane `l`'s double / vector, broadcast to every lane (exact: a bit copy via SGPRs).
+__device__ __forceinline__ double lane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ d3 lane_d3(d3 v, int l) {
+    return mk(lane_d(v.x, l), lane_d(v.y, l), lane_d(v.z, l));
+}
+
 struct SceneView {
     const double* sph;
     const double* pl;
@@ -145,14 +182,23 @@ __device__ __forceinline__ void bvh_triangles(const double* tri, const double* b
 
 // Scene::IntersectClosest: spheres, then planes, then triangles; a later candidate replaces
 // the current one only when strictly closer (HitInfo::isCloserThan, Shape.h:36).
-__device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) {
+// MASKED: only the spheres of `mask` (a wave-uniform set of spheres 0..63 that contains every
+// sphere the ray can hit, wf_shadow_mask), visited in ascending index order as the full loop
+// visits them, so ties resolve alike.
+template <bool MASKED>
+__device__ __forceinline__ bool closest_t(const SceneView& S, d3 o, d3 d, Hit& h, uint64_t mask) {
     bool found = false;
     double best = 0.0;
     int kind = 0, idx = -1;
     const double a = dot(d, d);       // Shape.h:75 (same value for every sphere)
     const double two_a = 2.0 * a;     // Shape.h:85-86 denominator
     const double four_a = 4.0 * a;    // Shape.h:79: (4.0 * a) * c
-    for (int i = 0; i < S.ns; ++i) {
+    for (int j = 0; MASKED ? mask != 0ull : j < S.ns; ++j) {
+        int i = j;
+        if constexpr (MASKED) {
+            i = __builtin_ctzll(mask);
+            mask &= mask - 1ull;
+        }
         const double* s = S.sph + kSphStride * i;
         const d3 oc = o - mk(s[0], s[1], s[2]);
         const double b = 2.0 * dot(oc, d);
@@ -213,6 +259,9 @@ __device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) 
     h.kind = kind;
     h.idx = idx;
     return found;
+}
+__device__ __forceinline__ bool closest(const SceneView& S, d3 o, d3 d, Hit& h) {
+    return closest_t<false>(S, o, d, h, 0ull);
 }
 
 // Image row of the launch's row-local row yl (contiguous, or block-cyclic for multi-GPU).
@@ -314,14 +363,18 @@ __device__ __forceinline__ d3 normal_of(const SceneView& S, const Hit& h, d3 p) 
     return mk(q[9], q[10], q[11]);
 }
 
-// Scene::computeTransmittance (Scene.h:35-77): closest-hit march of up to 64 steps.
-__device__ __forceinline__ double transmittance(const SceneView& S, d3 o, d3 d, double max_dist,
-                                                double bias) {
+// Scene::computeTransmittance (Scene.h:35-77): closest-hit march of up to 64 steps.  MASKED:
+// over the spheres of a shadow packet's capsule mask (wf_shadow_mask) — every sphere the march
+// can meet before the light is in it, and one it cannot meet only decides a step whose
+// closest hit lies beyond the light, where the march stops either way.
+template <bool MASKED>
+__device__ __forceinline__ double transmittance_t(const SceneView& S, d3 o, d3 d, double max_dist,
+                                                  double bias, uint64_t mask) {
     double T = 1.0, traveled = 0.0;
     int safety = 64;
     while (safety-- > 0 && T > 1e-4 && traveled < max_dist) {
         Hit h;
-        if (!closest(S, o, d, h)) break;
+        if (!closest_t<MASKED>(S, o, d, h, mask)) break;
         const double t = h.t;
         if (t <= 0.0) {
             o = o + d * bias;
@@ -339,6 +392,74 @@ __device__ __forceinline__ double transmittance(const SceneView& S, d3 o, d3 d, 
         traveled += t + bias;
     }
     return sclamp(T, 0.0, 1.0);
+}
+__device__ __forceinline__ double transmittance(const SceneView& S, d3 o, d3 d, double max_dist,
+                                                double bias) {
+    return transmittance_t<false>(S, o, d, max_dist, bias, 0ull);
+}
+
+// ------------------------------------------------------------------ shadow packets (direct pass)
+// The sphere mask of a wave's shadow rays towards one point light (the breadth-first renderer's
+// direct pass, rt_wavefront.hip; every lane calls it): the origins of the casting lanes lie in a
+// ball around the first one's origin (radius = the wave maximum of the FP32 distances, rounded
+// up), every ray runs from its origin towards the light point within the bias offset of its
+// segment (directLightning takes the direction from the hit point, the origin from P + n·bias),
+// so each ray of the march stays in the capsule of radius R + bias around [c, light].  Lane k
+// keeps sphere k unless its FP32 distance to that capsule clears the inflated radius by more than
+// the rounding slack (the packet kernel's cull_capsule test: 1e-4 relative radius margin, 2e-5
+// slack of the magnitudes, spheres with |C − c|/r > 1e5 always kept, NaN keeps).  Scenes with
+// more than 64 spheres, non-finite origins or radius: every sphere.
+constexpr float kShSlack = 2e-5f;
+constexpr float kShRel = 1e-4f;
+constexpr float kShFar = 1e5f;
+__device__ __forceinline__ float sh_f32_up(double v) {
+    return static_cast<float>(v) * (1.0f + 1e-6f);
+}
+__device__ __forceinline__ uint64_t wf_shadow_mask(const SceneView& S, bool casting, d3 so, d3 lpos,
+                                                   double bias) {
+    const uint64_t all = S.ns >= 64 ? ~0ull : ((1ull << S.ns) - 1ull);
+    const uint64_t cast = __ballot(casting);
+    if (!cast || S.ns > 64) return all;
+    const bool bad = casting && !(isfinite(so.x) && isfinite(so.y) && isfinite(so.z));
+    const d3 c = lane_d3(so, __builtin_ctzll(cast));
+    float r_lane = 0.0f;
+    if (casting) {  // |so − c| in FP32, rounded up (FP64 differences, 5e-7 relative error)
+        const float dx = static_cast<float>(so.x - c.x), dy = static_cast<float>(so.y - c.y),
+                    dz = static_cast<float>(so.z - c.z);
+        r_lane = __builtin_amdgcn_sqrtf(dx * dx + dy * dy + dz * dz) * (1.0f + 1e-5f);
+    }
+    const float R = wave_red<1>(r_lane);
+    if (__ballot(bad) || !isfinite(R) || !isfinite(lpos.x) || !isfinite(lpos.y) ||
+        !isfinite(lpos.z))
+        return all;
+    const float sx = static_cast<float>(lpos.x - c.x), sy = static_cast<float>(lpos.y - c.y),
+                sz = static_cast<float>(lpos.z - c.z);
+    const float sl2 = sx * sx + sy * sy + sz * sz;
+    const float inv_sl2 = 1.0f / sl2;  // only read when sl2 > 0
+    const float Rc = R + sh_f32_up(fabs(bias)) * 1.001f;  // |n| ≤ 1 + 2ε
+    const int k = static_cast<int>(threadIdx.x & 63u);
+    bool keep = false;
+    if (k < S.ns) {
+        const double* s = S.sph + kSphStride * k;
+        const float r = sh_f32_up(sqrt(s[3]));
+        const float vx = static_cast<float>(s[0] - c.x), vy = static_cast<float>(s[1] - c.y),
+                    vz = static_cast<float>(s[2] - c.z);
+        const float vs = vx * sx + vy * sy + vz * sz;
+        const float vv = vx * vx + vy * vy + vz * vz;
+        float d2;
+        if (!(vs > 0.0f) || !(sl2 > 0.0f)) {
+            d2 = vv;
+        } else if (!(vs < sl2)) {
+            const float wx = vx - sx, wy = vy - sy, wz = vz - sz;
+            d2 = wx * wx + wy * wy + wz * wz;
+        } else {
+            d2 = vv - (vs * vs) * inv_sl2;
+        }
+        const float lim = (r + Rc) * (1.0f + kShRel);
+        const float far = kShFar * r - Rc;
+        keep = !(d2 > lim * lim + kShSlack * (vv + sl2)) || !(far > 0.0f) || !(vv <= far * far);
+    }
+    return __ballot(keep);
 }
 
 // computeTransmittance for scenes without transparency (the direct and chain paths: any
@@ -444,6 +565,40 @@ __device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 vi
     }
 }
 
+// light_term for a whole wave (every lane calls it, `active` lanes shade): the shadow rays of the
+// wave's casting lanes share one capsule mask (wf_shadow_mask) and each march runs over it
+// (transmittance_t<true>) — the same steps, hits and T as light_term's march.
+template <bool COUNT>
+__device__ __forceinline__ void light_term_wave(const SceneView& S, bool active, d3 P, d3 n,
+                                                d3 view, const double* m, d3 lpos, d3 E,
+                                                double bias, d3& diff, d3& spec, Counts& cnt) {
+    double dist = 0.0, inv_d2 = 0.0;
+    d3 L = mk(0.0, 0.0, 0.0);
+    if (active) light_dir(lpos - P, dist, L, inv_d2);
+    bool need = active && !(dist <= 0.0);
+    double ndl = 0.0;
+    if (need) {
+        ndl = smax(0.0, dot(n, L));
+        need = !(ndl <= 0.0) && !(dist <= bias);
+    }
+    const d3 so = P + n * bias;
+    const uint64_t mask = wf_shadow_mask(S, need, so, lpos, bias);
+    if (!need) return;
+    if (COUNT) cnt.shadow++;
+    const double T = S.ns > 64 ? transmittance_t<false>(S, so, L, dist - bias, bias, 0ull)
+                               : transmittance_t<true>(S, so, L, dist - bias, bias, mask);
+    if (T <= bias) return;
+    diff = diff + ((E * inv_d2) * ndl) * T;
+    if (m[5] <= 0.0 && m[4] > 0.0) {  // transparency, specular
+        const d3 H = unit(L + view);
+        const double ndh = smax(0.0, dot(n, H));
+        if (ndh > 0.0) {
+            const double sf = pow_bp(ndh, m[3]);  // shininess
+            spec = spec + ((E * inv_d2) * sf) * T;
+        }
+    }
+}
+
 // Scene::directLightning (Scene.h:79-129), plus the build-defined area-light samples.
 template <bool COUNT, bool OPQ>
 __device__ __forceinline__ d3 direct(const SceneView& S, const TraceParams& P, d3 hp, d3 view,
@@ -491,20 +646,18 @@ struct Node {
 // `save` (the breadth-first level kernel, RT_WF_SAVE): this lane's hit point, shading normal and
 // incident direction are parked in LDS (structure of arrays, stride nthr) across the light loop
 // and read back for the child rays, so that their registers are free while the shadow rays run.
-template <bool TREE, bool COUNT>
-__device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, d3 o, d3 d,
-                                      uint64_t pix, uint32_t sample, int depth, Counts& cnt,
-                                      double* save = nullptr, int nthr = 0) {
+// shade_hit: TraceRay after its closest hit h (Scene.h:147-195).  DIRECT = false leaves out
+// directLightning (its value then lacks the local term: the breadth-first renderer's deferred
+// direct pass, rt_wavefront.hip, computes that term later from the same hit with DIRECT = true,
+// i.e. the same instructions on the same values); the child rays do not depend on it.
+// CHILDREN = false leaves out the child rays (that pass, for nodes whose children are traced).
+template <bool TREE, bool COUNT, bool DIRECT = true, bool CHILDREN = true>
+__device__ __forceinline__ Node shade_hit(const SceneView& S, const TraceParams& P, d3 o, d3 d,
+                                          const Hit& h, uint64_t pix, uint32_t sample, int depth,
+                                          Counts& cnt, double* save = nullptr, int nthr = 0) {
     Node nd;
     nd.refl = false;
     nd.refr = false;
-    if (COUNT) cnt.trace++;
-    Hit h;
-    if (!closest(S, o, d, h)) {
-        nd.hit = false;
-        nd.value = sky(d);
-        return nd;
-    }
     nd.hit = true;
     const double bias = P.bias;
     const d3 hp = o + d * h.t;  // Rayon::pointAtDistance
@@ -529,7 +682,8 @@ __device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, 
         save[8 * nthr] = inc.z;
         __asm__ volatile("" ::: "memory");  // no forwarding of the stored values
     }
-    const d3 local = direct<COUNT, !TREE>(S, P, hp, view, n, m, pix, sample, depth, cnt);
+    d3 local = mk(0.0, 0.0, 0.0);
+    if constexpr (DIRECT) local = direct<COUNT, !TREE>(S, P, hp, view, n, m, pix, sample, depth, cnt);
     d3 hp_c = hp, n_c = n, inc_c = inc;  // the values the child rays start from
     if (save) {
         __asm__ volatile("" ::: "memory");
@@ -538,8 +692,9 @@ __device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, 
         inc_c = mk(save[6 * nthr], save[7 * nthr], save[8 * nthr]);
     }
     d3 fin = mk(0.0, 0.0, 0.0);
-    if (tr < 1.0) fin = fin + local * (1.0 - tr);
+    if (DIRECT && tr < 1.0) fin = fin + local * (1.0 - tr);
     nd.value = fin;
+    if constexpr (!CHILDREN) return nd;
     double refl_w = m[4];
     if (TREE && tr > 0.0) {
         // fresnel (Scene.h:26-28, 161-164); only consumed when tr > 0.
@@ -571,6 +726,23 @@ __device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, 
         nd.rw = refl_w;
     }
     return nd;
+}
+
+template <bool TREE, bool COUNT>
+__device__ __forceinline__ Node shade(const SceneView& S, const TraceParams& P, d3 o, d3 d,
+                                      uint64_t pix, uint32_t sample, int depth, Counts& cnt,
+                                      double* save = nullptr, int nthr = 0) {
+    if (COUNT) cnt.trace++;
+    Hit h;
+    if (!closest(S, o, d, h)) {
+        Node nd;
+        nd.refl = false;
+        nd.refr = false;
+        nd.hit = false;
+        nd.value = sky(d);
+        return nd;
+    }
+    return shade_hit<TREE, COUNT>(S, P, o, d, h, pix, sample, depth, cnt, save, nthr);
 }
 
 // TraceRay for scenes where no secondary ray can be spawned.

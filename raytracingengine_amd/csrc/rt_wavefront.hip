@@ -21,6 +21,9 @@
 // is re-rendered by the per-pixel kernel (P.redo) in the same stream, so capacity never changes
 // the result.  No host synchronisation: the ray count of each level lives in device memory and
 // the level kernels are persistent grids that loop over it.
+#include <algorithm>
+#include <cstdlib>
+
 #include "rt_trace_common.hpp"
 #include "rt_wavefront.hpp"
 
@@ -85,14 +88,30 @@ constexpr int kWfLevelWaves = RT_WF_LEVEL_WAVES;
 #else
 constexpr int kWfLevelWaves = 2;
 #endif
-template <bool TREE, bool LDS>
-__global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(TraceParams P,
-                                                                             WfArena A, int level) {
+// Deferred direct lighting (the shadow stage, RTAMD_WF_DEFER, tree scenes): the level kernels
+// find each ray's closest hit and spawn its children, but leave directLightning — the light loop
+// and its computeTransmittance marches, 40 % of a glass frame spent at 57 % lane activity inside
+// the level kernels (profiles/r04_ab_glass_marches.txt, r04_glass_level_valu.json) — to
+// wf_direct_kernel, which shades every queued hit of every level in one launch with no other
+// work in its lanes.  Both run shade_hit (rt_trace_common.hpp) on the same hit, so the node
+// values are the same bits.
+constexpr uint32_t kDqIdxBits = 26;  // hit code: primitive index | kind << 26 | level << 28
+__device__ __forceinline__ uint32_t dq_code(const Hit& h, int level) {
+    return static_cast<uint32_t>(h.idx) | (static_cast<uint32_t>(h.kind) << kDqIdxBits) |
+           (static_cast<uint32_t>(level) << 28);
+}
+
+#ifndef RT_WF_DEFER_LEVEL_WAVES
+#define RT_WF_DEFER_LEVEL_WAVES 4
+#endif
+template <bool TREE, bool LDS, bool DEFER>
+__global__ __launch_bounds__(kWfThreads, DEFER ? RT_WF_DEFER_LEVEL_WAVES : kWfLevelWaves) void
+wf_level_kernel(TraceParams P, WfArena A, int level) {
     extern __shared__ double smem[];
     const SceneView S = stage_scene<LDS>(P, smem, threadIdx.x, kWfThreads);
 #if RT_WF_SAVE
     __shared__ double s_save[9 * kWfThreads];  // shade()'s parked hit point, normal, direction
-    double* const save = s_save + threadIdx.x;
+    double* const save = DEFER ? nullptr : s_save + threadIdx.x;
 #else
     double* const save = nullptr;
 #endif
@@ -109,16 +128,19 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
     const bool leaves = level + 1 >= P.max_rec;
     Counts cnt{0u, 0u};
 #if RT_WF_WG_ALLOC
-    // Child slots of level + 1 are reserved with ONE device atomic per workgroup and iteration
-    // (the four waves' counts summed in LDS): a single counter hit by every wave of the chip
-    // serialises at memory, one atomic per wave cost the deep levels most of their time.
+    // Child slots of level + 1 (and deferred-direct records) are reserved with ONE device atomic
+    // per workgroup and iteration (the four waves' counts summed in LDS): a single counter hit by
+    // every wave of the chip serialises at memory, one atomic per wave cost the deep levels most
+    // of their time.
     __shared__ uint32_t s_wtot[kWfThreads / 64], s_wbase;
+    __shared__ uint32_t s_dtot[kWfThreads / 64], s_dbase;
     const int wave = threadIdx.x >> 6;
     // workgroup-uniform grid-stride loop (the barriers below): every wave of the workgroup runs
     // every iteration, lanes past n idle (ballots below)
     for (uint32_t b0 = blockIdx.x * kWfThreads; b0 < n; b0 += gridDim.x * kWfThreads) {
         const uint32_t i = b0 + threadIdx.x;
 #else
+    static_assert(!DEFER, "the deferred direct queue is allocated per workgroup");
     // wave-uniform grid-stride loop: all 64 lanes run every iteration (ballots below)
     for (uint32_t i0 = blockIdx.x * kWfThreads + (threadIdx.x & ~63u); i0 < n;
          i0 += gridDim.x * kWfThreads) {
@@ -150,22 +172,62 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
         nd.refr = false;
         nd.fw = 0.0;
         nd.rw = 0.0;
+        bool defer = false;  // this node's local term is left to wf_direct_kernel
+        Hit h;
+        h.t = 0.0;
+        h.kind = 0;
+        h.idx = 0;
         if (active) {
-            if (level >= P.max_rec) nd.value = sky(d);  // TraceRay at depth >= maxRecursion
-            else nd = shade<TREE, false>(S, P, o, d, pix, sample, level, cnt, save, kWfThreads);
+            if (level >= P.max_rec) {
+                nd.value = sky(d);  // TraceRay at depth >= maxRecursion
+            } else if constexpr (DEFER) {
+                if (!closest(S, o, d, h)) {
+                    nd.value = sky(d);
+                } else {
+                    nd = shade_hit<TREE, false, false>(S, P, o, d, h, pix, sample, level, cnt);
+                    // fin = local·(1 − tr) only when tr < 1 (Scene.h:175-179): else no local term
+                    defer = sclamp(material_of(S, h)[5], 0.0, 1.0) < 1.0;
+                }
+            } else {
+                nd = shade<TREE, false>(S, P, o, d, pix, sample, level, cnt, save, kWfThreads);
+            }
         }
         const bool want_f = active && TREE && nd.hit && nd.refr;
         const bool want_r = active && nd.hit && nd.refl;
+        uint32_t dslot = 0;  // this lane's deferred record
+        if constexpr (DEFER) {
+            // one atomic per workgroup for the deferred records of its four waves, in wave order
+            const uint64_t bd = __ballot(defer);
+            if (lane == 0) s_dtot[wave] = __builtin_popcountll(bd);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const uint32_t sum = s_dtot[0] + s_dtot[1] + s_dtot[2] + s_dtot[3];
+                s_dbase = sum ? atomicAdd(leaves ? &A.ctl->dleaf : &A.ctl->dcount, sum) : 0u;
+            }
+            __syncthreads();
+            dslot = s_dbase + lane_prefix(bd);
+            for (int w = 0; w < wave; ++w) dslot += s_dtot[w];
+            __syncthreads();  // s_dtot / s_dbase are rewritten by the next iteration
+            if (leaves) dslot = A.cap - 1u - dslot;  // the last level's records from the back
+            if (defer) {  // at most one record per node: the queue holds cap records
+                A.dq_id[dslot] = id;
+                A.dq_code[dslot] = dq_code(h, level);
+                A.dq_t[dslot] = h.t;
+            }
+        }
         if (leaves) {  // uniform: children at depth maxRecursion are the sky (Scene.h:132-134)
-            if (active) {
+            if (active && !defer) {
                 // the fold of this node with those children, in the reference's order
-                // (Scene.h:176-195): (local + refraction·fw) + reflection·rw
+                // (Scene.h:176-195): (local + refraction·fw) + reflection·rw (a deferred node is
+                // folded by wf_direct_kernel once its local term is known)
                 d3 v = nd.value;
                 if (want_f) v = v + sky(nd.fd) * nd.fw;
                 if (want_r) v = v + sky(nd.rd) * nd.rw;
                 A.val[id] = v.x;
                 A.val[A.cap + id] = v.y;
                 A.val[2 * A.cap + id] = v.z;
+            }
+            if (active) {
                 A.child[id] = -1;
                 A.child[A.cap + id] = -1;
             }
@@ -233,14 +295,133 @@ __global__ __launch_bounds__(kWfThreads, kWfLevelWaves) void wf_level_kernel(Tra
             A.ctl->lost = 1u;
         }
         if (active) {
-            A.val[id] = nd.value.x;
-            A.val[A.cap + id] = nd.value.y;
-            A.val[2 * A.cap + id] = nd.value.z;
+            if (!defer) {  // a deferred node's value is written by wf_direct_kernel
+                A.val[id] = nd.value.x;
+                A.val[A.cap + id] = nd.value.y;
+                A.val[2 * A.cap + id] = nd.value.z;
+            }
             A.fw[id] = nd.fw;
             A.rw[id] = nd.rw;
             A.child[id] = cf;
             A.child[A.cap + id] = cr;
         }
+    }
+}
+
+// The deferred direct lighting of every level's queued hits: shade_hit with directLightning
+// (the same function and values as a level kernel's own shade), the node's value written, and at
+// the last shading level its fold with the sky children (as the level kernel does for the nodes
+// it shades itself).  Persistent grid over the queue; the records of a workgroup are consecutive
+// nodes of one level, so a wave's hits stay as coherent as the level kernel's were.
+#ifndef RT_WF_DIRECT_WAVES
+#define RT_WF_DIRECT_WAVES 4
+#endif
+template <bool TREE, bool LDS, bool LEAF>
+__global__ __launch_bounds__(kWfThreads, RT_WF_DIRECT_WAVES) void wf_direct_kernel(TraceParams P,
+                                                                                   WfArena A) {
+    extern __shared__ double smem[];
+    const SceneView S = stage_scene<LDS>(P, smem, threadIdx.x, kWfThreads);
+    // the inner levels' records [0, dcount), the last level's [cap − dleaf, cap)
+    const uint32_t n = min(LEAF ? A.ctl->dleaf : A.ctl->dcount, A.cap);
+    const uint32_t q0 = LEAF ? A.cap - n : 0u;
+    const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    const uint32_t aa = static_cast<uint32_t>(P.aa);
+    const double bias = P.bias;
+    const int lane = threadIdx.x & 63;
+    Counts cnt{0u, 0u};
+    // wave-uniform grid-stride loop: every lane takes part in the shadow packets' ballots
+    for (uint32_t i0 = blockIdx.x * kWfThreads + (threadIdx.x & ~63u); i0 < n;
+         i0 += gridDim.x * kWfThreads) {
+        const uint32_t qi = i0 + lane;
+        const bool active = qi < n;
+        const uint32_t q = q0 + (active ? qi : 0u);
+        uint32_t id = 0;
+        Hit h;
+        h.t = 0.0;
+        h.kind = 1;
+        h.idx = 0;
+        d3 o = mk(0.0, 0.0, 0.0), d = mk(0.0, 0.0, 1.0);
+        uint64_t pix = 0;
+        uint32_t sample = 0;
+        int level = 0;
+        if (active) {
+            id = A.dq_id[q];
+            const uint32_t code = A.dq_code[q];
+            h.t = A.dq_t[q];
+            h.idx = static_cast<int>(code & ((1u << kDqIdxBits) - 1u));
+            h.kind = static_cast<int>((code >> kDqIdxBits) & 3u);
+            level = static_cast<int>(code >> 28);
+            uint32_t root;
+            if (id < A.n0) {  // a camera ray: the level kernel's own getRay
+                root = id;
+                const uint32_t pl = root / aa, s = root % aa;
+                const uint32_t x = pl % P.width, y = image_row(P, pl / P.width);
+                o = cam;
+                d = camera_dir(P, cam, x, y, static_cast<uint64_t>(y) * P.width + x,
+                               static_cast<int>(s));
+            } else {
+                const size_t r = id - A.n0;
+                root = A.root[r];
+                o = mk(A.ray[r], A.ray[A.cap_r + r], A.ray[2 * A.cap_r + r]);
+                d = mk(A.ray[3 * A.cap_r + r], A.ray[4 * A.cap_r + r], A.ray[5 * A.cap_r + r]);
+            }
+            const uint32_t pl = root / aa;
+            sample = root % aa;
+            pix = static_cast<uint64_t>(image_row(P, pl / P.width)) * P.width + pl % P.width;
+        }
+        // shade_hit's shading inputs (Scene.h:147-154) and directLightning (Scene.h:79-129)
+        // with one shadow packet per light for the wave
+        const d3 hp = o + d * h.t;  // Rayon::pointAtDistance
+        d3 nn = mk(0.0, 1.0, 0.0), view = mk(0.0, 0.0, 0.0);
+        const double* m = S.sph_mat;
+        if (active) {
+            const d3 gn = normal_of(S, h, hp);
+            m = material_of(S, h);
+            const d3 inc = unit(d);
+            const bool front = dot(gn, inc) < 0.0;
+            view = -inc;
+            nn = unit(front ? gn : -gn);  // directLightning's own normalize (Scene.h:81)
+        }
+        d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
+        for (int l = 0; l < S.nl; ++l) {
+            const double* lt = S.lt + kLtStride * l;
+            light_term_wave<false>(S, active, hp, nn, view, m, mk(lt[0], lt[1], lt[2]),
+                                   mk(lt[3], lt[4], lt[5]), bias, diff, spec, cnt);
+        }
+#ifndef RT_LEAN_GENERIC  // the build-defined area light: per-lane sample points, full marches
+        if (active && P.al_samples > 0) {
+            const uint32_t stream = 0x10000u + (sample << 6) + static_cast<uint32_t>(level);
+            const double k = static_cast<double>(P.al_k);
+            const d3 corner = mk(P.al_corner[0], P.al_corner[1], P.al_corner[2]);
+            const d3 eu = mk(P.al_u[0], P.al_u[1], P.al_u[2]);
+            const d3 ev = mk(P.al_v[0], P.al_v[1], P.al_v[2]);
+            const d3 E = mk(P.al_E[0], P.al_E[1], P.al_E[2]);
+            for (int s = 0; s < P.al_samples; ++s) {
+                const double r1 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(s));
+                const double r2 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(s) + 1u);
+                const double fu = (static_cast<double>(s % P.al_k) + r1) / k;
+                const double fv = (static_cast<double>(s / P.al_k) + r2) / k;
+                const d3 lp = (corner + eu * fu) + ev * fv;
+                light_term<false, false>(S, hp, nn, view, m, lp, E, bias, diff, spec, cnt);
+            }
+        }
+#endif
+        if (!active) continue;
+        const d3 local = hmul(mk(m[0], m[1], m[2]), diff) + spec * m[4];
+        const double tr = sclamp(m[5], 0.0, 1.0);
+        d3 v = mk(0.0, 0.0, 0.0);
+        if (tr < 1.0) v = v + local * (1.0 - tr);  // Scene.h:175-179 (fin)
+        if constexpr (LEAF) {
+            // the last shading level: fold with the sky children (the child rays of the same hit,
+            // shade_hit without directLightning)
+            const Node nd = shade_hit<TREE, false, false, true>(S, P, o, d, h, pix, sample, level,
+                                                                cnt);
+            if (TREE && nd.refr) v = v + sky(nd.fd) * nd.fw;
+            if (nd.refl) v = v + sky(nd.rd) * nd.rw;
+        }
+        A.val[id] = v.x;
+        A.val[A.cap + id] = v.y;
+        A.val[2 * A.cap + id] = v.z;
     }
 }
 
@@ -286,7 +467,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_final_kernel(TraceParams P, WfA
     store_pixel(P, p, v);
 }
 
-template <bool TREE, bool LDS>
+template <bool TREE, bool LDS, bool DEFER>
 hipError_t launch_levels(const TraceParams& p, const WfArena& A, size_t lds_bytes,
                          hipStream_t stream) {
     const int max_level = p.max_rec > 0 ? p.max_rec : 0;
@@ -301,17 +482,30 @@ hipError_t launch_levels(const TraceParams& p, const WfArena& A, size_t lds_byte
         cus <= 0)
         cus = 256;
     const size_t rounds = (A.cap_r + kWfThreads - 1) / kWfThreads;
-    const uint32_t gk = static_cast<uint32_t>(
-        std::min<size_t>(static_cast<size_t>(cus) * kWfLevelWaves, rounds));
     const uint32_t gf = static_cast<uint32_t>(std::min<size_t>(static_cast<size_t>(cus) * 8, rounds));
     const size_t lds = LDS ? lds_bytes : 0;
+    const uint32_t waves = DEFER ? RT_WF_DEFER_LEVEL_WAVES : kWfLevelWaves;
+    const uint32_t gk = static_cast<uint32_t>(
+        std::min<size_t>(static_cast<size_t>(cus) * waves, rounds));
     if (g0 > 0)
-        hipLaunchKernelGGL((wf_level_kernel<TREE, LDS>), dim3(g0), dim3(kWfThreads), lds, stream,
-                           p, A, 0);
+        hipLaunchKernelGGL((wf_level_kernel<TREE, LDS, DEFER>), dim3(g0), dim3(kWfThreads), lds,
+                           stream, p, A, 0);
     // levels 1 .. maxRecursion − 1 (depth maxRecursion is folded in by the last of them)
     for (int k = 1; k < max_level && gk > 0; ++k)
-        hipLaunchKernelGGL((wf_level_kernel<TREE, LDS>), dim3(gk), dim3(kWfThreads), lds, stream,
-                           p, A, k);
+        hipLaunchKernelGGL((wf_level_kernel<TREE, LDS, DEFER>), dim3(gk), dim3(kWfThreads), lds,
+                           stream, p, A, k);
+    if constexpr (DEFER) {
+        // every level's deferred hits: one resident round of workgroups over the queue
+        const size_t qrounds = (A.cap + kWfThreads - 1) / kWfThreads;
+        const uint32_t gd = static_cast<uint32_t>(
+            std::min<size_t>(static_cast<size_t>(cus) * RT_WF_DIRECT_WAVES, qrounds));
+        if (max_level > 1 && gd > 0)  // the inner levels' hits
+            hipLaunchKernelGGL((wf_direct_kernel<TREE, LDS, false>), dim3(gd), dim3(kWfThreads),
+                               lds, stream, p, A);
+        if (max_level > 0 && gd > 0)  // the last shading level's hits, folded with the sky
+            hipLaunchKernelGGL((wf_direct_kernel<TREE, LDS, true>), dim3(gd), dim3(kWfThreads),
+                               lds, stream, p, A);
+    }
     // folds of levels maxRecursion − 2 .. 1 (the last shading level folded its nodes itself)
     for (int k = max_level - 2; k >= 1 && gf > 0; --k)
         hipLaunchKernelGGL(wf_fold_kernel, dim3(gf), dim3(kWfThreads), 0, stream, A, k);
@@ -328,7 +522,7 @@ hipError_t launch_levels(const TraceParams& p, const WfArena& A, size_t lds_byte
 #ifndef RT_LEAN_GENERIC
 size_t wf_arena_bytes(size_t n0, size_t cap) {
     const size_t cap_r = cap - n0;
-    return sizeof(double) * (5 * cap + 6 * cap_r) + sizeof(int32_t) * 2 * cap +
+    return sizeof(double) * (6 * cap + 6 * cap_r) + sizeof(int32_t) * 4 * cap +
            sizeof(uint32_t) * cap_r + n0 + 64;
 }
 
@@ -346,10 +540,16 @@ WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl) {
     q += sizeof(double) * cap;
     A.ray = reinterpret_cast<double*>(q);
     q += sizeof(double) * 6 * A.cap_r;
+    A.dq_t = reinterpret_cast<double*>(q);
+    q += sizeof(double) * cap;
     A.child = reinterpret_cast<int32_t*>(q);
     q += sizeof(int32_t) * 2 * cap;
     A.root = reinterpret_cast<uint32_t*>(q);
     q += sizeof(uint32_t) * A.cap_r;
+    A.dq_id = reinterpret_cast<uint32_t*>(q);
+    q += sizeof(uint32_t) * cap;
+    A.dq_code = reinterpret_cast<uint32_t*>(q);
+    q += sizeof(uint32_t) * cap;
     A.redo = reinterpret_cast<uint8_t*>(q);
     A.ctl = ctl;
     return A;
@@ -361,12 +561,23 @@ hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bo
     hipError_t e = hipMemsetAsync(A.ctl, 0, sizeof(WfCtl), stream);
     if (e == hipSuccess && A.n0 > 0) e = hipMemsetAsync(A.redo, 0, A.n0, stream);
     if (e != hipSuccess) return e;
-    if (path == kPathTree)
-        e = lds ? launch_levels<true, true>(p, A, lds_bytes, stream)
-                : launch_levels<true, false>(p, A, lds_bytes, stream);
+    // deferred direct lighting for refraction trees (RTAMD_WF_DEFER=1; off by default: measured
+    // on glass 994 vs 971 us per frame, the level kernels 848 -> 480 us but the direct pass 390 us,
+    // profiles/r05_glass_defer.txt)
+    const char* defer_env = std::getenv("RTAMD_WF_DEFER");  // read per frame (tests switch it)
+    const bool defer = defer_env && std::atoi(defer_env) == 1;
+    // (the queue's hit code holds a primitive index below 2^26 and a level below 16)
+    static_assert(kMaxDepth <= 16, "dq_code level bits");
+    const bool fits = p.ns < (1 << 26) && p.np < (1 << 26) && p.nt < (1 << 26);
+    if (path == kPathTree && defer && fits)
+        e = lds ? launch_levels<true, true, true>(p, A, lds_bytes, stream)
+                : launch_levels<true, false, true>(p, A, lds_bytes, stream);
+    else if (path == kPathTree)
+        e = lds ? launch_levels<true, true, false>(p, A, lds_bytes, stream)
+                : launch_levels<true, false, false>(p, A, lds_bytes, stream);
     else
-        e = lds ? launch_levels<false, true>(p, A, lds_bytes, stream)
-                : launch_levels<false, false>(p, A, lds_bytes, stream);
+        e = lds ? launch_levels<false, true, false>(p, A, lds_bytes, stream)
+                : launch_levels<false, false, false>(p, A, lds_bytes, stream);
     if (e != hipSuccess) return e;
     // fix-up: the per-pixel kernel for pixels whose sample trees overflowed the arena (the lean
     // build's own, rtamd::lean::launch_trace)

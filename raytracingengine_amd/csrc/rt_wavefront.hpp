@@ -14,6 +14,8 @@ struct WfCtl {
     uint32_t count[kMaxDepth + 2];
     uint32_t base[kMaxDepth + 2];
     uint32_t lost;  // some sample's tree overflowed the arena (the fix-up pass has work)
+    uint32_t dcount;  // deferred direct-lighting records of the inner levels (queue front)
+    uint32_t dleaf;   // ... of the last shading level (queue back, filled backwards)
 };
 
 // Node ids [0, n0) are the roots (pixel samples, row-local pixel * aa + sample); deeper nodes
@@ -26,6 +28,13 @@ struct WfArena {
     int32_t* child;   // 2 x cap: refraction child id, reflection child id (−1: none)
     uint32_t* root;   // cap_r: root id of node n0 + r
     uint8_t* redo;    // n0: 1 = the tree of this root overflowed the arena
+    // deferred direct lighting (the shadow stage): one record per hit node with transparency
+    // < 1, appended by the level kernels — node id, hit code (primitive index | kind << 26 |
+    // level << 28), hit distance — and shaded by wf_direct_kernel after the last level; the
+    // last shading level's records fill the queue from the back
+    uint32_t* dq_id;    // cap
+    uint32_t* dq_code;  // cap
+    double* dq_t;       // cap
     WfCtl* ctl;
     uint32_t n0, cap, cap_r;
 };

@@ -950,3 +950,36 @@ def test_generic_sample_parallel_equals_per_thread_loop(ctx, name, flags, aa):
     assert np.array_equal(out["hdr64"], ref["hdr64"])
     assert np.array_equal(out["ldr"], ref["ldr"])
     assert (out["trace_rays"], out["shadow_rays"]) == (ref["trace_rays"], ref["shadow_rays"])
+
+
+@pytest.mark.parametrize("variant,aa,max_rec", [("glass", 1, 10), ("glass", 3, 6), ("glass", 1, 1),
+                                                ("glass", 1, 2), ("glass", 1, 16),
+                                                ("glass_area_tris", 1, 10)])
+def test_wavefront_deferred_direct_equals_in_level(ctx, monkeypatch, variant, aa, max_rec):
+    """The shadow stage (RTAMD_WF_DEFER=1, opt-in): the level kernels queue every hit with
+    transparency < 1 and wf_direct_kernel shades them after the last level (the light loop and
+    its computeTransmittance marches, plus the fold with the sky children at the last shading
+    level).  Bit-identical to the level kernels shading in place (RTAMD_WF_DEFER=0) and to the
+    per-pixel DFS kernel, for AA, depth 1 (every root a leaf), 2, 10 and 16, and for the full
+    build's level kernels (a transparent scene with triangles and the area light)."""
+    sc = make_config("glass", 160, 90, aa=aa)
+    if variant == "glass_area_tris":
+        from raytracingengine_amd.scene import AreaLight, Material
+        sc.add_triangle((-4.0, -3.0, 6.0), (4.0, -3.0, 6.0), (0.0, 4.0, 7.0),
+                        Material((0.8, 0.7, 0.6), specular=0.2, transparency=0.5,
+                                 refractive_index=1.3))
+        sc.area_light = AreaLight((-3.0, 12.0, -8.0), (6.0, 0.0, 0.0), (0.0, 0.0, 6.0),
+                                  (1.0, 1.0, 1.0), 150.0, 4)
+    ds = ctx.scene(sc)
+    try:
+        outs = {}
+        for defer in ("1", "0"):
+            monkeypatch.setenv("RTAMD_WF_DEFER", defer)
+            outs[defer] = ds.render(hdr64=True, tonemap=1, max_recursion=max_rec)
+        ref = ds.render(hdr64=True, tonemap=1, max_recursion=max_rec,
+                        flags=capi.RT_FLAG_GENERIC_KERNEL)
+    finally:
+        ds.close()
+    for k in ("1", "0"):
+        assert np.array_equal(outs[k]["hdr64"], ref["hdr64"], equal_nan=True), k
+        assert np.array_equal(outs[k]["ldr"], ref["ldr"]), k
