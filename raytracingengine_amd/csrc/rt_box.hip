@@ -1,6 +1,7 @@
-// rt_box.hip — reflection chains of scenes made of planes only (no spheres, triangles or area
+// rt_box.hip — reflection chains of scenes made of planes and spheres (no triangles or area
 // light): the reference main()'s own scene (RaytracingEngine.cpp:255-291, BASELINE config 1 — a
-// box of five axis-aligned mirrored walls lit by two point lights) and any box-like room.
+// box of five axis-aligned mirrored walls lit by two point lights), any box-like room, and rooms
+// with up to 64 spheres in them (the SPH instantiations: the mirror scene).
 //
 // Same TraceRay chain as trace_chain (rt_trace_common.hpp: Scene.h:131-198 with transparency 0,
 // accumulated front to back), same shading helpers, so the image is bit-identical to the generic
@@ -20,8 +21,11 @@
 //  * Shadow rays are classified (blocked / clear / undecided) from the same A = num·sign(denom),
 //    B = |denom| as the generic occlusion_opaque, which for such a plane are sign(d_k)·(p_k − o_k)
 //    and |d_k| exactly; undecided lanes run the exact computeTransmittance march.
+//  * Spheres (SPH) are read through the scalar cache as well and tested first, in scene order,
+//    with the reference's literal Sphere::Intersect (Shape.h:72-98) — IntersectClosest visits
+//    spheres before planes (Scene.h:221-241).
 // Closest-hit ties between groups keep the reference's order: the lower scene index wins
-// (strict '<' in scene order, Shape.h:36 / Scene.h:233-241).
+// (strict '<' in scene order, Shape.h:36 / Scene.h:233-241), every sphere before every plane.
 #include "rt_trace_common.hpp"
 
 #pragma clang fp contract(off)
@@ -43,14 +47,17 @@ struct BoxScene {
     cdp pl;           // box table, kBoxRec doubles per plane, in group order
     const double* g;  // the same table for per-lane (vector) reads of the hit plane
     cdp lt;           // point lights (kLtStride)
+    cdp sph;          // spheres (kSphStride: cx cy cz r²), SPH instantiations
+    const double* sph_v;  // the same for per-lane reads of the hit sphere
+    const double* mat;    // material table [spheres | planes] (per-lane reads)
     int n[4];         // planes per group: normal ±e_x, ±e_y, ±e_z, any other
-    int nl;
+    int nl, ns;
 };
 
 struct BoxHit {
     double t;
-    int rec;   // the hit plane's record (group order)
-    int orig;  // its scene index
+    int rec;   // the hit plane's record (group order), or −1 − i for sphere i
+    int orig;  // its position in IntersectClosest's order: sphere i, then ns + plane index
 };
 
 // |o_i| ≤ 2^1000 (with the table's |p_i| ≤ 2^1000 every p_i − o_i is finite, so the shortcut's
@@ -63,7 +70,8 @@ __device__ __forceinline__ bool box_ray_ok(d3 o, d3 d) {
 }
 
 __device__ __forceinline__ double comp(d3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
-__device__ __forceinline__ int rec_orig(cdp q) { return __double2loint(q[15]); }
+// a plane record's position in IntersectClosest's order (after the spheres)
+__device__ __forceinline__ int rec_orig(const BoxScene& S, cdp q) { return S.ns + __double2loint(q[15]); }
 
 // The reference's literal Plane::Intersect quotient (Shape.h:149-159); denom checked by the caller.
 __device__ __forceinline__ double plane_literal_t(cdp q, d3 o, d3 d) {
@@ -99,7 +107,7 @@ __device__ __forceinline__ void box_group_closest(const BoxScene& S, int first, 
         if (__ballot(odd)) {  // uniform: some lane needs the literal quotient
             if (odd) t = c == 0.0 ? plane_literal_t(q, o, d) : c / dk;
         }
-        if (live) box_take(t, first + j, rec_orig(q), found, h);
+        if (live) box_take(t, first + j, rec_orig(S, q), found, h);
     }
 }
 
@@ -113,17 +121,56 @@ __device__ __forceinline__ void box_literal_closest(const BoxScene& S, int first
         const double denom = dot(nn, d);
         if (fabs(denom) > 1e-6) {
             const double t = dot(mk(q[0], q[1], q[2]) - o, nn) / denom;
-            box_take(t, first + j, rec_orig(q), found, h);
+            box_take(t, first + j, rec_orig(S, q), found, h);
         }
     }
 }
 
-// Scene::IntersectClosest over the planes (Scene.h:218-257; Plane::Intersect Shape.h:149-159).
+// IntersectClosest's sphere loop (Scene.h:221-232; Sphere::Intersect Shape.h:72-98, literal),
+// sphere records through the scalar cache.
+__device__ __forceinline__ void box_spheres_closest(const BoxScene& S, d3 o, d3 d, bool& found,
+                                                    BoxHit& h) {
+    const double a = dot(d, d);       // Shape.h:75 (same value for every sphere)
+    const double two_a = 2.0 * a;     // Shape.h:85-86 denominator
+    const double four_a = 4.0 * a;    // Shape.h:79: (4.0 * a) * c
+    for (int i = 0; i < S.ns; ++i) {
+        cdp s = S.sph + kSphStride * i;
+        const d3 oc = o - mk(s[0], s[1], s[2]);
+        const double b = 2.0 * dot(oc, d);
+        const double c = dot(oc, oc) - s[3];
+        const double disc = b * b - four_a * c;
+        if (disc < 0.0) continue;
+        const double sq = sqrt(disc);
+        double t0 = (-b - sq) / two_a;
+        double t1 = (-b + sq) / two_a;
+        if (t0 > t1) {
+            const double tmp = t0;
+            t0 = t1;
+            t1 = tmp;
+        }
+        double t = t0;
+        if (t < 1e-6) {
+            t = t1;
+            if (t < 1e-6) continue;
+        }
+        if (!found || t < h.t) {
+            found = true;
+            h.t = t;
+            h.rec = -1 - i;
+            h.orig = i;
+        }
+    }
+}
+
+// Scene::IntersectClosest (Scene.h:218-257): the spheres (SPH), then the planes (Plane::Intersect
+// Shape.h:149-159).
+template <bool SPH>
 __device__ __forceinline__ bool box_closest(const BoxScene& S, d3 o, d3 d, BoxHit& h) {
     bool found = false;
     h.t = 0.0;
     h.rec = 0;
     h.orig = 0;
+    if constexpr (SPH) box_spheres_closest(S, o, d, found, h);
     const int g1 = S.n[0], g2 = g1 + S.n[1], g3 = g2 + S.n[2];
     if (__ballot(!box_ray_ok(o, d)) == 0) {  // uniform
         box_group_closest<0>(S, 0, o, d, found, h);
@@ -175,11 +222,59 @@ __device__ __forceinline__ void box_literal_occlusion(const BoxScene& S, int fir
     }
 }
 
-// computeTransmittance (Scene.h:35-77) of an opaque planes-only scene: 1 clear, 0 blocked, -1
-// undecided (the exact march decides).
+// The spheres' part of occlusion_opaque (rt_trace_common.hpp): hit / miss by the reference's FP64
+// discriminant, the roots within an explicit error bound from a FP32 square root and one shared
+// reciprocal of 2a; anything near a threshold is undecided.
+__device__ __forceinline__ void box_spheres_occlusion(const BoxScene& S, d3 o, d3 d,
+                                                      double max_dist, double bias, bool& blocked,
+                                                      bool& undecided) {
+    const double a = dot(d, d);
+    const double two_a = 2.0 * a, four_a = 4.0 * a;
+    if (!(two_a >= 0x1p-100 && two_a <= 0x1p100)) {
+        undecided = true;
+        return;
+    }
+    const double inv2a = rcp_refined(two_a);  // within 1 ulp of 1/2a: far inside the Δ margin
+    for (int i = 0; i < S.ns; ++i) {
+        cdp s = S.sph + kSphStride * i;
+        const d3 oc = o - mk(s[0], s[1], s[2]);
+        const double b = 2.0 * dot(oc, d);
+        const double cc = dot(oc, oc) - s[3];
+        const double disc = b * b - four_a * cc;
+        if (disc < 0.0) continue;  // miss, exactly as the reference decides it
+        if (!(disc == 0.0 || (disc > 1e-30 && disc < 1e30))) {
+            undecided = true;
+            continue;
+        }
+        // |sq − fl(√disc)| ≤ 5e-7·√disc, so both roots are within Δ of the reference's
+        const double sq = static_cast<double>(__builtin_amdgcn_sqrtf(static_cast<float>(disc)));
+        const double delta = 2e-6 * (fabs(b) + sq) * inv2a;
+        double t = (-b - sq) * inv2a;
+        if (!(t >= 1e-6 + delta)) {
+            if (!(t < 1e-6 - delta)) {
+                undecided = true;
+                continue;
+            }
+            t = (-b + sq) * inv2a;
+            if (t < 1e-6 - delta) continue;
+            if (!(t >= 1e-6 + delta)) {
+                undecided = true;
+                continue;
+            }
+        }
+        if (t >= max_dist + delta) continue;
+        if (t > bias + delta && t < max_dist - delta) blocked = true;
+        else undecided = true;
+    }
+}
+
+// computeTransmittance (Scene.h:35-77) of an opaque scene of planes (and spheres): 1 clear, 0
+// blocked, -1 undecided (the exact march decides).
+template <bool SPH>
 __device__ __forceinline__ int box_occlusion(const BoxScene& S, d3 o, d3 d, double max_dist,
                                              double bias) {
     bool blocked = false, undecided = false;
+    if constexpr (SPH) box_spheres_occlusion(S, o, d, max_dist, bias, blocked, undecided);
     const int g1 = S.n[0], g2 = g1 + S.n[1], g3 = g2 + S.n[2];
     if (__ballot(!box_ray_ok(o, d)) == 0) {  // uniform
         box_group_occlusion<0>(S, 0, o, d, max_dist, bias, blocked, undecided);
@@ -192,14 +287,20 @@ __device__ __forceinline__ int box_occlusion(const BoxScene& S, d3 o, d3 d, doub
     return undecided ? -1 : (blocked ? 0 : 1);
 }
 
-// The exact march (transmittance(), rt_trace_common.hpp) over the planes.
+// The hit's material record (r g b shininess specular transparency ior).
+__device__ __forceinline__ const double* box_material(const BoxScene& S, const BoxHit& h) {
+    return h.rec < 0 ? S.mat + kMatStride * (-1 - h.rec) : S.g + kBoxRec * h.rec + 8;
+}
+
+// The exact march (transmittance(), rt_trace_common.hpp).
+template <bool SPH>
 __device__ __forceinline__ double box_transmittance(const BoxScene& S, d3 o, d3 d,
                                                     double max_dist, double bias) {
     double T = 1.0, traveled = 0.0;
     int safety = 64;
     while (safety-- > 0 && T > 1e-4 && traveled < max_dist) {
         BoxHit h;
-        if (!box_closest(S, o, d, h)) break;
+        if (!box_closest<SPH>(S, o, d, h)) break;
         const double t = h.t;
         if (t <= 0.0) {
             o = o + d * bias;
@@ -212,16 +313,16 @@ __device__ __forceinline__ double box_transmittance(const BoxScene& S, d3 o, d3 
             continue;
         }
         if (traveled + t >= max_dist) break;
-        T *= sclamp(S.g[kBoxRec * h.rec + 13], 0.0, 1.0);
+        T *= sclamp(box_material(S, h)[5], 0.0, 1.0);
         o = (o + d * t) + d * bias;
         traveled += t + bias;
     }
     return sclamp(T, 0.0, 1.0);
 }
 
-// One TraceRay level (shade<false>, rt_trace_common.hpp) for a planes-only opaque scene:
-// the local light of the hit (or the sky) and the reflection ray.
-template <bool COUNT>
+// One TraceRay level (shade<false>, rt_trace_common.hpp) for an opaque scene of planes (and
+// spheres): the local light of the hit (or the sky) and the reflection ray.
+template <bool COUNT, bool SPH>
 __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& P, d3 o, d3 d,
                                           Counts& cnt) {
     Node nd;
@@ -229,7 +330,7 @@ __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& 
     nd.refr = false;
     if (COUNT) cnt.trace++;
     BoxHit h;
-    if (!box_closest(S, o, d, h)) {
+    if (!box_closest<SPH>(S, o, d, h)) {
         nd.hit = false;
         nd.value = sky(d);
         return nd;
@@ -237,10 +338,18 @@ __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& 
     nd.hit = true;
     const double bias = P.bias;
     const d3 hp = o + d * h.t;  // Rayon::pointAtDistance
-    const double* r = S.g + kBoxRec * h.rec;
-    const d3 gn = mk(r[3], r[4], r[5]);  // Plane::GetNormalAt (Shape.h:161-163)
-    const bool unit_n = r[7] != 0.0;     // |n| rounds to exactly 1: normalize() returns n
-    const Mat m = load_mat(r + 8);
+    d3 gn;
+    bool unit_n;
+    if (SPH && h.rec < 0) {  // Sphere::GetNormalAt (Shape.h:100-102)
+        const double* c = S.sph_v + kSphStride * (-1 - h.rec);
+        gn = unit(hp - mk(c[0], c[1], c[2]));
+        unit_n = false;
+    } else {
+        const double* r = S.g + kBoxRec * h.rec;
+        gn = mk(r[3], r[4], r[5]);  // Plane::GetNormalAt (Shape.h:161-163)
+        unit_n = r[7] != 0.0;       // |n| rounds to exactly 1: normalize() returns n
+    }
+    const Mat m = load_mat(box_material(S, h));
     const d3 inc = unit(d);
     const bool front = dot(gn, inc) < 0.0;
     const d3 n0 = front ? gn : -gn;
@@ -261,9 +370,9 @@ __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& 
         if (dist <= bias) continue;
         if (COUNT) cnt.shadow++;
         const d3 so = hp + n * bias;
-        const int occ = box_occlusion(S, so, L, dist - bias, bias);
+        const int occ = box_occlusion<SPH>(S, so, L, dist - bias, bias);
         const double T = occ >= 0 ? static_cast<double>(occ)
-                                  : box_transmittance(S, so, L, dist - bias, bias);
+                                  : box_transmittance<SPH>(S, so, L, dist - bias, bias);
         if (T <= bias) continue;
         diff = diff + ((E * inv_d2) * ndl) * T;
         if (m.transparency <= 0.0 && m.specular > 0.0) {
@@ -291,7 +400,7 @@ __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& 
 
 // One sample of GeneratePixelAt (Scene.h:283-304): TraceRay as a reflection chain accumulated
 // front to back (trace_chain's order, so the image equals the generic chain kernel's bit for bit).
-template <bool COUNT>
+template <bool COUNT, bool SPH>
 __device__ __forceinline__ d3 box_sample(const BoxScene& S, const TraceParams& P, d3 cam,
                                          uint32_t x, uint32_t y, uint64_t pix, int s, Counts& cnt) {
     d3 d = camera_dir(P, cam, x, y, pix, s);
@@ -303,7 +412,7 @@ __device__ __forceinline__ d3 box_sample(const BoxScene& S, const TraceParams& P
             c = c + sky(d) * w;
             break;
         }
-        const Node nd = box_shade<COUNT>(S, P, o, d, cnt);
+        const Node nd = box_shade<COUNT, SPH>(S, P, o, d, cnt);
         c = c + nd.value * w;
         if (!nd.hit || !nd.refl) break;
         w = w * nd.rw;
@@ -318,8 +427,12 @@ __device__ __forceinline__ BoxScene box_scene(const TraceParams& P) {
     S.pl = (cdp)P.box;
     S.g = P.box;
     S.lt = (cdp)P.lt;
-    for (int k = 0; k < 4; ++k) S.n[k] = P.box_n[k];
+    S.sph = (cdp)P.sph;
+    S.sph_v = P.sph;
+    S.mat = P.sph_mat;
+    for (int k = 0; k < 4; ++k) S.n[k] = P.box ? P.box_n[k] : 0;
     S.nl = P.nl;
+    S.ns = P.ns;
     return S;
 }
 
@@ -345,7 +458,7 @@ __device__ __forceinline__ void box_count(const Counts& cnt, const TraceParams& 
 // divides by the sample count: the same operations in the same order as the per-thread loop.
 constexpr int kBoxAaThreads = 256;
 constexpr int kBoxAaMax = 128;  // larger sample counts keep the per-thread loop
-template <bool COUNT>
+template <bool COUNT, bool SPH>
 __global__ __launch_bounds__(kBoxAaThreads, RT_BOX_WAVES) void box_aa_kernel(TraceParams P) {
     __shared__ double s_c[3 * kBoxAaThreads];
     const int tid = threadIdx.x;
@@ -361,7 +474,7 @@ __global__ __launch_bounds__(kBoxAaThreads, RT_BOX_WAVES) void box_aa_kernel(Tra
         const uint32_t y = image_row(P, static_cast<uint32_t>(lin / P.width));
         const uint64_t pix = static_cast<uint64_t>(y) * P.width + x;
         const d3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-        const d3 c = box_sample<COUNT>(S, P, cam, x, y, pix, s, cnt);
+        const d3 c = box_sample<COUNT, SPH>(S, P, cam, x, y, pix, s, cnt);
         s_c[tid] = c.x;
         s_c[kBoxAaThreads + tid] = c.y;
         s_c[2 * kBoxAaThreads + tid] = c.z;
@@ -381,7 +494,7 @@ __global__ __launch_bounds__(kBoxAaThreads, RT_BOX_WAVES) void box_aa_kernel(Tra
 
 // GeneratePixelAt (Scene.h:283-304) with a per-thread sample loop: single-sample frames, and
 // sample counts of 0 or above kBoxAaMax.
-template <bool COUNT, bool SINGLE>
+template <bool COUNT, bool SINGLE, bool SPH>
 __global__ __launch_bounds__(kTileW * kTileH, SINGLE ? RT_BOX_WAVES : RT_BOX_MULTI_WAVES) void box_chain_kernel(TraceParams P) {
     const uint32_t x = blockIdx.x * kTileW + threadIdx.x;
     const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
@@ -395,7 +508,7 @@ __global__ __launch_bounds__(kTileW * kTileH, SINGLE ? RT_BOX_WAVES : RT_BOX_MUL
         int samples = 0;
         const int nsamples = SINGLE ? 1 : P.aa;
         for (int s = 0; s < nsamples; ++s) {
-            acc = acc + box_sample<COUNT>(S, P, cam, x, y, pix, s, cnt);
+            acc = acc + box_sample<COUNT, SPH>(S, P, cam, x, y, pix, s, cnt);
             samples += 1;
         }
         const d3 v = samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0);
@@ -404,26 +517,35 @@ __global__ __launch_bounds__(kTileW * kTileH, SINGLE ? RT_BOX_WAVES : RT_BOX_MUL
     if constexpr (COUNT) box_count<COUNT>(cnt, P, threadIdx.y * kTileW + threadIdx.x);
 }
 
-hipError_t launch_box_chain(const TraceParams& p, bool count, bool sample_parallel,
-                            hipStream_t stream) {
+template <bool SPH>
+static hipError_t launch_box(const TraceParams& p, bool count, bool sample_parallel,
+                             hipStream_t stream) {
     if (sample_parallel && p.aa >= 2 && p.aa <= kBoxAaMax) {
         const int ppw = kBoxAaThreads / p.aa;
         const uint64_t npx = static_cast<uint64_t>(p.width) * p.rows;
         const dim3 grid(static_cast<unsigned>((npx + ppw - 1) / ppw));
-        if (count) hipLaunchKernelGGL((box_aa_kernel<true>), grid, dim3(kBoxAaThreads), 0, stream, p);
-        else hipLaunchKernelGGL((box_aa_kernel<false>), grid, dim3(kBoxAaThreads), 0, stream, p);
+        if (count) hipLaunchKernelGGL((box_aa_kernel<true, SPH>), grid, dim3(kBoxAaThreads), 0, stream, p);
+        else hipLaunchKernelGGL((box_aa_kernel<false, SPH>), grid, dim3(kBoxAaThreads), 0, stream, p);
         return hipGetLastError();
     }
     const dim3 block(kTileW, kTileH);
     const dim3 grid((p.width + kTileW - 1) / kTileW, (p.rows + kTileH - 1) / kTileH);
     if (count) {
-        if (p.aa == 1) hipLaunchKernelGGL((box_chain_kernel<true, true>), grid, block, 0, stream, p);
-        else hipLaunchKernelGGL((box_chain_kernel<true, false>), grid, block, 0, stream, p);
+        if (p.aa == 1) hipLaunchKernelGGL((box_chain_kernel<true, true, SPH>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((box_chain_kernel<true, false, SPH>), grid, block, 0, stream, p);
     } else {
-        if (p.aa == 1) hipLaunchKernelGGL((box_chain_kernel<false, true>), grid, block, 0, stream, p);
-        else hipLaunchKernelGGL((box_chain_kernel<false, false>), grid, block, 0, stream, p);
+        if (p.aa == 1) hipLaunchKernelGGL((box_chain_kernel<false, true, SPH>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((box_chain_kernel<false, false, SPH>), grid, block, 0, stream, p);
     }
     return hipGetLastError();
+}
+
+hipError_t launch_box_chain(const TraceParams& p, bool count, bool sample_parallel,
+                            hipStream_t stream) {
+    if (p.nt != 0 || p.al_samples != 0 || p.ns > kBoxMaxSpheres || (p.np > 0 && !p.box))
+        return hipErrorInvalidValue;  // the launcher's conditions (rt_capi.cpp)
+    return p.ns > 0 ? launch_box<true>(p, count, sample_parallel, stream)
+                    : launch_box<false>(p, count, sample_parallel, stream);
 }
 
 }  // namespace rtamd

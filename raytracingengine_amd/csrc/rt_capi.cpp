@@ -617,9 +617,16 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
     }
     // generic kernels without triangle / area-light code for scenes that use neither
     const bool lean_generic = p.nt == 0 && p.al_samples == 0;
-    // reflection chains of scenes made of planes only take the planes-only chain kernel
-    const bool box = path == kPathChain && p.ns == 0 && p.nt == 0 && p.al_samples == 0 &&
-                     p.np > 0 && !(flags & RT_FLAG_GENERIC_KERNEL);
+    // reflection chains of scenes made of planes (and up to kBoxMaxSpheres spheres) take the
+    // scalar-cache chain kernel (rt_box.hip); RTAMD_BOX_SPH=0 keeps scenes with spheres on the
+    // generic chain kernel (A/B runs)
+    static const bool box_sph = [] {
+        const char* e = std::getenv("RTAMD_BOX_SPH");
+        return !(e && std::atoi(e) == 0);
+    }();
+    const bool box = path == kPathChain && p.nt == 0 && p.al_samples == 0 &&
+                     (p.ns == 0 ? p.np > 0 : (box_sph && p.ns <= kBoxMaxSpheres)) &&
+                     !(flags & RT_FLAG_GENERIC_KERNEL);
     const bool spar = !(flags & RT_FLAG_NO_SAMPLE_PARALLEL);
     auto launch = [&](const TraceParams& q, bool count) {
         if (box)

@@ -21,6 +21,7 @@ constexpr int kMatStride = 8;   // r g b shininess specular transparency ior -
 // p xyz | n xyz | p[k] (k = the group's axis) | 1 when |n| rounds to exactly 1 |
 // material (kMatStride - 1 doubles: r g b shininess specular transparency ior) | scene index (int)
 constexpr int kBoxRec = 16;
+constexpr int kBoxMaxSpheres = 64;  // reflection chains with spheres take rt_box.hip up to this
 
 constexpr int kBvhNodeStride = 8;  // triangle BVH node: lo xyz, hi xyz, {first, count}
 constexpr int kBvhMinTris = 32;    // scenes with fewer triangles test them all (no BVH)

@@ -928,7 +928,8 @@ def test_box_sample_parallel_equals_per_thread_loop(ctx, aa):
     assert np.array_equal(part["hdr64"], rows)
 
 
-@pytest.mark.parametrize("name,flags", [("mirror", 0), ("mesh", 0),
+@pytest.mark.parametrize("name,flags", [("mirror", 0), ("mirror", capi.RT_FLAG_GENERIC_KERNEL),
+                                        ("mesh", 0),
                                         ("c1", capi.RT_FLAG_GENERIC_KERNEL),
                                         ("c2", capi.RT_FLAG_GENERIC_KERNEL),
                                         ("c5", capi.RT_FLAG_GENERIC_KERNEL)])
@@ -983,3 +984,44 @@ def test_wavefront_deferred_direct_equals_in_level(ctx, monkeypatch, variant, aa
     for k in ("1", "0"):
         assert np.array_equal(outs[k]["hdr64"], ref["hdr64"], equal_nan=True), k
         assert np.array_equal(outs[k]["ldr"], ref["ldr"]), k
+
+
+def _sphere_room(kind):
+    """Scenes for the sphere instantiations of rt_box.hip: the mirror scene (12 spheres in a
+    mirrored box), its spheres without the walls, and the mirror spheres around the camera (one
+    sphere containing the camera: camera rays start inside it)."""
+    import copy
+    sc = make_config("mirror", 160, 90)
+    if kind == "no_planes":
+        sc = copy.deepcopy(sc)
+        sc.planes = []
+    elif kind == "camera_inside":
+        from raytracingengine_amd.scene import Material
+        sc = copy.deepcopy(sc)
+        sc.add_sphere((0.0, 0.0, -25.0), 3.0, Material((0.5, 0.6, 0.7), shininess=16.0,
+                                                       specular=0.5))
+    return sc
+
+
+@pytest.mark.parametrize("kind,aa,max_rec", [("mirror", 1, 10), ("mirror", 3, 4), ("mirror", 1, 1),
+                                             ("mirror", 1, 16), ("no_planes", 1, 10),
+                                             ("camera_inside", 1, 10), ("mirror", 32, 10)])
+def test_box_spheres_equal_generic_chain(ctx, kind, aa, max_rec):
+    """Reflection chains with spheres through rt_box.hip (spheres and axis-grouped planes read
+    through the scalar cache, every sphere tested first in scene order with the literal
+    Sphere::Intersect, then the planes' shortcut): every pixel, the ACES bytes and the ray counts
+    bit-identical to the generic chain kernel — depth 1 to 16, AA (sample-parallel and the
+    per-thread loop), a scene without planes and a camera inside a sphere."""
+    sc = _sphere_room(kind)
+    if aa != 1:
+        sc = sc.resized(sc.camera.width, sc.camera.height, aa)
+    out = _render(ctx, sc, hdr64=True, tonemap=6, stats=True, max_recursion=max_rec)
+    ref = _render(ctx, sc, hdr64=True, tonemap=6, stats=True, max_recursion=max_rec,
+                  flags=capi.RT_FLAG_GENERIC_KERNEL)
+    assert np.array_equal(out["hdr64"], ref["hdr64"], equal_nan=True)
+    assert np.array_equal(out["ldr"], ref["ldr"])
+    assert (out["trace_rays"], out["shadow_rays"]) == (ref["trace_rays"], ref["shadow_rays"])
+    if aa > 1:
+        loop = _render(ctx, sc, hdr64=True, tonemap=6, max_recursion=max_rec,
+                       flags=capi.RT_FLAG_NO_SAMPLE_PARALLEL)
+        assert np.array_equal(out["hdr64"], loop["hdr64"], equal_nan=True)
