@@ -126,61 +126,15 @@ __device__ __forceinline__ void box_literal_closest(const BoxScene& S, int first
     }
 }
 
-// IntersectClosest's sphere loop (Scene.h:221-232; Sphere::Intersect Shape.h:72-98), sphere
-// records through the scalar cache.  When every lane's 2a lies in [2^-100, 2^100] (unit
-// reflection and camera rays) the roots take the packet kernel's exact forms (rt_packet.hip
-// sphere_roots_core: the sqrt / division cores with one shared reciprocal of 2a, the far root
-// only when the near one is below 1e-6 — t0 ≤ t1 holds exactly for 2a > 0 — and no division when
-// the near root provably cannot be strictly closer than the best so far); otherwise the literal
-// expressions.  RT_BOX_SPH_FAST=0: the literal loop only (A/B).
-#ifndef RT_BOX_SPH_FAST
-#define RT_BOX_SPH_FAST 1
-#endif
+// IntersectClosest's sphere loop (Scene.h:221-232; Sphere::Intersect Shape.h:72-98, literal),
+// sphere records through the scalar cache.  (The packet kernel's exact root forms — sqrt /
+// division cores with a shared reciprocal of 2a, lazy far root, no-win skip — were 2 % slower
+// here: mirror 1.352 vs 1.325 ms, profiles/r05_ab_box_spheres.txt.)
 __device__ __forceinline__ void box_spheres_closest(const BoxScene& S, d3 o, d3 d, bool& found,
                                                     BoxHit& h) {
     const double a = dot(d, d);       // Shape.h:75 (same value for every sphere)
     const double two_a = 2.0 * a;     // Shape.h:85-86 denominator
     const double four_a = 4.0 * a;    // Shape.h:79: (4.0 * a) * c
-#if RT_BOX_SPH_FAST
-    if (__ballot(!(two_a >= 0x1p-100 && two_a <= 0x1p100)) == 0) {  // uniform
-        const double r2a = rcp_refined(two_a);
-        for (int i = 0; i < S.ns; ++i) {
-            cdp s = S.sph + kSphStride * i;
-            const d3 oc = o - mk(s[0], s[1], s[2]);
-            const double b = 2.0 * dot(oc, d);
-            const double c = dot(oc, oc) - s[3];
-            const double disc = b * b - four_a * c;
-            if (disc < 0.0) continue;
-            double t;
-            if (disc >= 0x1p-767 && disc <= 0x1.fffffffffffffp+1023) {
-                const double sq = sqrt_core(disc);
-                const double n0 = -b - sq;
-                // t1 ≥ t0 > best (strictly): neither root can win (spheres come first, so a
-                // found best is a sphere root ≥ 1e-6 > 0)
-                if (found && n0 > (h.t * two_a) * (1.0 + 0x1.0p-40)) continue;
-                t = div_core(n0, two_a, r2a);
-                if (t < 1e-6) {
-                    t = div_core(-b + sq, two_a, r2a);
-                    if (t < 1e-6) continue;
-                }
-            } else {
-                const double sq = sqrt(disc);
-                t = (-b - sq) / two_a;
-                if (t < 1e-6) {
-                    t = (-b + sq) / two_a;
-                    if (t < 1e-6) continue;
-                }
-            }
-            if (!found || t < h.t) {
-                found = true;
-                h.t = t;
-                h.rec = -1 - i;
-                h.orig = i;
-            }
-        }
-        return;
-    }
-#endif
     for (int i = 0; i < S.ns; ++i) {
         cdp s = S.sph + kSphStride * i;
         const d3 oc = o - mk(s[0], s[1], s[2]);
