@@ -580,7 +580,9 @@ def main(argv=None):
     traffic_launch = None
     if traffic and R.world == 1:
         traffic_launch = traffic["hbm_bytes_per_launch"] / 32 * frames_per_launch
-    valu, valu_src = load_profile(f"r04_{args.config}_valu.json")
+    valu, valu_src = load_profile(f"r05_{args.config}_valu.json")
+    if valu is None:
+        valu, valu_src = load_profile(f"r04_{args.config}_valu.json")
     if valu is None:
         valu, valu_src = load_profile(f"r03_{args.config}_valu.json")
     line = {

@@ -514,13 +514,35 @@ bool uses_wavefront_arena(int path, int flags) {
 }
 
 rt_status scratch_wait(rt_context* ctx) {
-    if (ctx->scratch_used) RT_HIP(hipStreamWaitEvent(ctx->stream, ctx->scratch_event, 0));
+    // the latest user on this same stream is ordered before us already
+    if (ctx->scratch_used && ctx->scratch_stream != ctx->stream)
+        RT_HIP(hipStreamWaitEvent(ctx->stream, ctx->scratch_event, 0));
     return RT_OK;
 }
 
 rt_status scratch_done(rt_context* ctx) {
     RT_HIP(hipEventRecord(ctx->scratch_event, ctx->stream));
     ctx->scratch_used = true;
+    ctx->scratch_stream = ctx->stream;
+    return RT_OK;
+}
+
+// The packet kernel's fix-up buffers for a launch of `px` output pixels (rt_internal.hpp
+// TraceParams.fix_list): the list grows on demand, the two control words are zeroed once (every
+// fix-up launch leaves them zero).
+rt_status fixup_buffers(rt_context* ctx, size_t px, TraceParams& p) {
+    if (px >= (size_t(1) << 32)) return fail(RT_ERR_UNSUPPORTED, "fix-up list above 2^32 pixels");
+    if (!ctx->fix_ctl.ptr) {
+        RT_HIP(ctx->fix_ctl.ensure(2 * sizeof(uint32_t)));
+        RT_HIP(hipMemsetAsync(ctx->fix_ctl.ptr, 0, 2 * sizeof(uint32_t), ctx->stream));
+    }
+    if (ctx->fix_list.bytes < px * sizeof(uint32_t)) {
+        // the list may still be read by a fix-up launch on any stream the context used
+        RT_HIP(hipDeviceSynchronize());
+        RT_HIP(ctx->fix_list.ensure(px * sizeof(uint32_t)));
+    }
+    p.fix_list = static_cast<uint32_t*>(ctx->fix_list.ptr);
+    p.fix_ctl = static_cast<uint32_t*>(ctx->fix_ctl.ptr);
     return RT_OK;
 }
 
@@ -579,11 +601,7 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
         }
         return RT_OK;
     }
-    const bool scratch = (flags & RT_FLAG_COUNT_RAYS) || uses_wavefront_arena(path, flags);
-    if (scratch) {
-        st = scratch_wait(ctx);
-        if (st != RT_OK) return st;
-    }
+    bool scratch = (flags & RT_FLAG_COUNT_RAYS) || uses_wavefront_arena(path, flags);
 
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (flags & RT_FLAG_TIME_KERNEL) {
@@ -613,6 +631,19 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
         if (st != RT_OK) return st;
     } else if (packet) {
         st = packet_image(ctx, sc, p, flags, &rec);
+        if (st != RT_OK) return st;
+    }
+    // the fix-up variant of the packet kernel (undecided shadow rays re-rendered per pixel after
+    // the launch) uses the context's fix-up list: ordered across streams like the counters
+    const bool fixup = packet && packet_uses_fixup(p, false, sc->max_specular > 0.0);
+    if (fixup) {
+        st = fixup_buffers(ctx, nframes > 1 ? static_cast<size_t>(nframes) * frame_px
+                                             : static_cast<size_t>(rows) * p.width, p);
+        if (st != RT_OK) return st;
+        scratch = true;
+    }
+    if (scratch) {
+        st = scratch_wait(ctx);
         if (st != RT_OK) return st;
     }
     // generic kernels without triangle / area-light code for scenes that use neither
@@ -662,6 +693,7 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
         }
     }
     if (!wavefront) RT_HIP(launch(p, false));
+    if (fixup) RT_HIP(launch_packet_fixup(p, ctx->stream));
     if (rec) RT_HIP(hipEventRecord(rec->recorded, ctx->stream));
     if (flags & RT_FLAG_TIME_KERNEL) {
         RT_HIP(hipEventRecord(ev.second, ctx->stream));
@@ -753,7 +785,8 @@ rt_status rt_context_destroy(rt_context* ctx) {
     }
     leave_groups(ctx);  // communicators of any group this context is in go first
     for (DeviceBuffer* b : {&ctx->out64, &ctx->out32, &ctx->ldr, &ctx->tm_in, &ctx->tm_out,
-                            &ctx->dbg, &ctx->rays, &ctx->counters, &ctx->wf, &ctx->wf_ctl})
+                            &ctx->dbg, &ctx->rays, &ctx->counters, &ctx->wf, &ctx->wf_ctl,
+                            &ctx->fix_list, &ctx->fix_ctl})
         b->release();
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;

@@ -71,6 +71,10 @@ struct rt_context {
     // previous one that did, on whatever stream it ran (scratch_wait / scratch_done).
     hipEvent_t scratch_event = nullptr;
     bool scratch_used = false;
+    hipStream_t scratch_stream = nullptr;  // the stream of the latest scratch user
+    // the packet kernel's fix-up list (TraceParams.fix_list) and its control words, one per
+    // context like the counters (ordered across streams by scratch_wait / scratch_done)
+    rtamd::DeviceBuffer fix_list, fix_ctl;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
     double timed_ms = 0.0;

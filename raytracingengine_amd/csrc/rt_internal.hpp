@@ -108,6 +108,12 @@ struct TraceParams {
     // normal ±e_x, ±e_y, ±e_z, any other
     const double* box;
     int32_t box_n[4];
+    // packet kernel, fix-up variants (kFeatFix): undecided shadow rays are not marched; the
+    // pixel's output index (frame · frame_px + row-local pixel) is appended to fix_list and
+    // packet_fixup_kernel renders it with the exact per-pixel path.  fix_ctl: [0] count,
+    // [1] workgroups of the fix-up launch done (its last workgroup zeroes both)
+    uint32_t* fix_list;
+    uint32_t* fix_ctl;
     // packet kernel frame batch: nframes > 0 replaces cam_pos / pk_image / pk_pub / pk_epoch
     // by fr[blockIdx.z]; frame z writes its outputs frame_px pixels after frame z - 1's
     uint32_t nframes;
@@ -147,6 +153,10 @@ hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specu
                                 hipStream_t stream);
 size_t packet_lds_bytes(int ns, int np, int nl);
 hipError_t launch_packet_image(const TraceParams& p, double* img, hipStream_t stream);
+// Whether launch_packet_direct takes a fix-up variant for p (then p.fix_list / p.fix_ctl must be
+// set, with room for every output pixel of the launch), and the fix-up launch that follows it.
+bool packet_uses_fixup(const TraceParams& p, bool count, bool any_specular);
+hipError_t launch_packet_fixup(const TraceParams& p, hipStream_t stream);
 // The images a frame batch forms before its launch: job j forms frame frame[j]'s image
 // (camera p.fr[frame[j]].cam) at dst[j] — a cache entry of the scene or a slot of its ring.
 struct PkImageJobs {

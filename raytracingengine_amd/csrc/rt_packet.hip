@@ -26,6 +26,8 @@
 //    fires).
 //  * Shadow-ray marches (computeTransmittance, Scene.h:35-77) only move the origin along the
 //    segment towards the light, so one capsule mask serves the whole march.
+#include <cstdlib>
+
 #include "rt_trace_common.hpp"
 
 #pragma clang fp contract(off)
@@ -69,6 +71,15 @@ constexpr int kFeatAll = 31;
 // plane and point-light code compiles away; the single-sample instantiation then runs at 6
 // waves/SIMD (80 VGPRs): C5 508 -> 490 us at 5 waves, -> 482 us at 6 (MI355X)
 constexpr int kFeatNoPL = 32;
+// Fix-up variant (with no other feature; single sample, ≤ 64 spheres: C2): a lane whose shadow
+// ray the classifier leaves undecided does not march (computeTransmittance's exact loop is not
+// compiled in, which takes the variant from 80 VGPRs + 44 B/lane of spills at 6 waves/SIMD to 64
+// VGPRs + 12 B at 8); its pixel is queued instead and packet_fixup_kernel renders it with the
+// exact per-pixel path after the launch (0.08 % of C2's shadow rays are undecided).
+constexpr int kFeatFix = 128;
+#ifndef RT_PACKET_FIX_WAVES
+#define RT_PACKET_FIX_WAVES 8
+#endif
 
 // Waves per SIMD of the single-sample variant for <= 64 spheres, point lights and no other
 // feature (C2): 6 with its light records read through the scalar cache (80 VGPRs, 48 B/lane of
@@ -806,7 +817,8 @@ template <int MAXC, int FEAT, bool COUNT>
 __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P, d3 n, d3 view,
                                          const PkHit& h, d3 lpos, d3 E, d3 lcenter, double lrad,
                                          double bias, int nchunks, d3& diff, d3& spec,
-                                         Counts& cnt, const Masks<MAXC>* pre = nullptr) {
+                                         Counts& cnt, const Masks<MAXC>* pre = nullptr,
+                                         bool* fix = nullptr) {
     double dist = 0.0, inv_d2 = 0.0;
     d3 L = mk(0.0, 0.0, 0.0);
     if (active) light_dir(lpos - P, dist, L, inv_d2);  // skipped by waves with no hit lane
@@ -893,7 +905,10 @@ __device__ __forceinline__ void pk_light(const PacketScene& S, bool active, d3 P
     // row split went from 1.37-1.45× the mean rank to 1.02-1.04× (profiles/r02_*).
     const bool undecided = need && occ == 2;
     double T = occ == 1 ? 0.0 : 1.0;
-    if (__ballot(undecided)) {  // uniform
+    if constexpr ((FEAT & kFeatFix) != 0) {
+        // no march here: the pixel is queued for packet_fixup_kernel (its output is rewritten)
+        if (undecided) *fix = true;
+    } else if (__ballot(undecided)) {  // uniform
         Masks<MAXC> Mu = M;
         const OriginBall Bu = origin_ball(undecided, so);
         if (Bu.ok) {
@@ -1022,7 +1037,8 @@ __device__ __forceinline__ void pk_build_image(const TraceParams& P, const doubl
 
 // Waves per SIMD of a variant (its register budget).
 constexpr int pk_waves(int MAXC, int FEAT, bool COUNT, bool MULTI) {
-    return (FEAT == 0 && MAXC == 1 && !MULTI && !COUNT) ? RT_PACKET_SMALL_WAVES
+    return (FEAT == kFeatFix && MAXC == 1 && !MULTI && !COUNT) ? RT_PACKET_FIX_WAVES
+         : (FEAT == 0 && MAXC == 1 && !MULTI && !COUNT) ? RT_PACKET_SMALL_WAVES
          : (FEAT == (kFeatArea | kFeatNoPL) && !MULTI && !COUNT) ? RT_PACKET_AREA_WAVES
          : FEAT == kFeatTris ? RT_PACKET_TRIS_WAVES
          : (((FEAT == 0 || (FEAT & ~kFeatNoPL) == kFeatArea || FEAT == kFeatPlanes) && MAXC <= 4)
@@ -1169,6 +1185,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, pk_waves(MAXC, FEAT, COUNT, M
         al_r = (0.5 * (length(eu) + length(ev))) * (1.0 + kCullRel);
     }
     Counts cnt{0u, 0u};
+    bool fix = false;  // kFeatFix: an undecided shadow ray, the pixel goes to the fix-up
 
     d3 acc = mk(0.0, 0.0, 0.0);
     int samples = 0;
@@ -1262,7 +1279,7 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, pk_waves(MAXC, FEAT, COUNT, M
                     nl_ = mk(park[3 * kThreads], park[4 * kThreads], park[5 * kThreads]);
                 }
                 pk_light<MAXC, FEAT, COUNT>(S, hit, hl, nl_, view, h, L, E, L, 0.0, bias, nchunks,
-                                            diff, spec, cnt);
+                                            diff, spec, cnt, nullptr, &fix);
             }
             if constexpr ((FEAT & kFeatArea) != 0) {
                 if (P.al_samples > 0) {
@@ -1351,7 +1368,26 @@ __global__ __launch_bounds__(64 * kWgWavesX * WGY, pk_waves(MAXC, FEAT, COUNT, M
     const uint32_t wave_e = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wave));
     const uint32_t x_e = tbx * (kPkW * kWgWavesX) + (wave_e % kWgWavesX) * kPkW + (lane_e % kPkW);
     const uint32_t yl_e = tby * (kPkH * WGY) + (wave_e / kWgWavesX) * kPkH + (lane_e / kPkW);
-    if (x_e < P.width && yl_e < P.rows) {
+    bool store = x_e < P.width && yl_e < P.rows;
+    if constexpr ((FEAT & kFeatFix) != 0) {
+        // the pixels with an undecided shadow ray: appended to the fix-up list (one atomic per
+        // wave), rendered by packet_fixup_kernel after this launch instead of stored here
+        const bool q = fix && store;
+        const uint64_t bq = __ballot(q);
+        if (bq) {
+            uint32_t base = 0;
+            if (lane_e == static_cast<uint32_t>(__builtin_ctzll(bq)))
+                base = atomicAdd(P.fix_ctl, static_cast<uint32_t>(__builtin_popcountll(bq)));
+            base = __shfl(base, __builtin_ctzll(bq), 64);
+            if (q)
+                P.fix_list[base + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bq >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo(
+                                                                static_cast<uint32_t>(bq), 0u))] =
+                    static_cast<uint32_t>(frame_off + static_cast<size_t>(yl_e) * P.width + x_e);
+        }
+        store = store && !fix;
+    }
+    if (store) {
         // accumulated / samples (Scene.h:298-300); x / 1.0 == x, so AA=1 skips the division
         const d3 v = samples == 1 ? acc
                    : (samples > 0 ? sdiv(acc, static_cast<double>(samples)) : mk(0.0, 0.0, 0.0));
@@ -1436,6 +1472,61 @@ hipError_t launch_packet_image_batch(const TraceParams& p, const PkImageJobs& jo
             return hipErrorInvalidValue;
     hipLaunchKernelGGL(packet_image_batch_kernel, dim3(static_cast<unsigned>(jobs.n)),
                        dim3(256), 0, stream, p, jobs);
+    return hipGetLastError();
+}
+
+// The pixels a fix-up variant queued (TraceParams.fix_list: output index frame · frame_px + row-
+// local pixel): GeneratePixelAt (Scene.h:283-304) with one sample through the per-pixel path —
+// generic closest hit over every primitive, occlusion_opaque and the exact computeTransmittance
+// march (rt_trace_common.hpp trace_direct) — the same image bits as the packet kernel, stored
+// like it.  A persistent grid over the device-side count; its last workgroup zeroes the count
+// for the next launch (no memset on the stream).
+constexpr int kFixThreads = 256;
+__global__ __launch_bounds__(kFixThreads) void packet_fixup_kernel(TraceParams P) {
+    const uint32_t n = __hip_atomic_load(P.fix_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    SceneView S;
+    S.ns = P.ns;
+    S.np = P.np;
+    S.nt = P.nt;
+    S.nl = P.nl;
+    S.sph = P.sph;
+    S.pl = P.pl;
+    S.lt = P.lt;
+    S.tri = P.tri;
+    S.sph_mat = P.sph_mat;
+    S.pl_mat = P.pl_mat;
+    S.tri_mat = P.tri_mat;
+    S.bvh = P.bvh;
+    S.bvh_tri = P.bvh_tri;
+    Counts cnt{0u, 0u};
+    for (uint32_t i = blockIdx.x * kFixThreads + threadIdx.x; i < n; i += gridDim.x * kFixThreads) {
+        const uint64_t o = P.fix_list[i];
+        const uint32_t z = P.nframes ? static_cast<uint32_t>(o / P.frame_px) : 0u;
+        const uint64_t pl = o - static_cast<uint64_t>(z) * (P.nframes ? P.frame_px : 0u);
+        const uint32_t yl = static_cast<uint32_t>(pl / P.width);
+        const uint32_t x = static_cast<uint32_t>(pl - static_cast<uint64_t>(yl) * P.width);
+        const double* cp = P.nframes ? P.fr[z].cam : P.cam_pos;
+        const d3 cam = mk(cp[0], cp[1], cp[2]);
+        const uint32_t y = image_row(P, yl);
+        const uint64_t pix = static_cast<uint64_t>(y) * P.width + x;
+        const d3 d = camera_dir(P, cam, x, y, pix, 0);
+        d3 acc = mk(0.0, 0.0, 0.0);
+        acc = acc + trace_direct<false>(S, P, cam, d, pix, 0u, cnt);  // one sample (AA = 1)
+        store_pixel(P, static_cast<size_t>(o), acc);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(P.fix_ctl + 1, 1u) == gridDim.x - 1) {  // every workgroup has read n
+            __hip_atomic_store(P.fix_ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(P.fix_ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+hipError_t launch_packet_fixup(const TraceParams& p, hipStream_t stream) {
+    if (!p.fix_list || !p.fix_ctl) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(packet_fixup_kernel, dim3(256), dim3(kFixThreads), 0, stream, p);
     return hipGetLastError();
 }
 
@@ -1588,16 +1679,14 @@ static void launch_packet_maxc(const TraceParams& p, bool count, size_t lds, int
     // compiled feature sets: lean (the BASELINE C2-C4 shape), lean + plane culls (C3), lean +
     // area light (C5, rt_packet_area.hip), triangles / models only (no Blinn-Phong, area light
     // or Reinhard-Jodie), and everything
-    if (feat == 0) launch_packet_variant<MAXC, 0>(p, count, lds, stream);
+    if (feat == kFeatFix) launch_packet_variant<1, kFeatFix>(p, count, lds, stream);
+    else if (feat == 0) launch_packet_variant<MAXC, 0>(p, count, lds, stream);
     else if (feat == kFeatPlanes) launch_packet_variant<MAXC, kFeatPlanes>(p, count, lds, stream);
     else if (feat == kFeatTris) launch_packet_variant<MAXC, kFeatTris>(p, count, lds, stream);
     else launch_packet_variant<MAXC, kFeatAll>(p, count, lds, stream);
 }
 
-hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specular,
-                                hipStream_t stream) {
-    const size_t lds = packet_lds_bytes(p.ns, p.np, p.nl);
-    const int chunks = (p.ns + 63) / 64;
+static int packet_features(const TraceParams& p, bool any_specular) {
     int feat = 0;
     if (any_specular) feat |= kFeatSpec;
     if (p.al_samples > 0) feat |= kFeatArea;
@@ -1605,6 +1694,31 @@ hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specu
     if (p.ldr && p.tonemap == 4) feat |= kFeatJodie;
     // the plane cull has its own lean variant; combined with other features the general one
     if (p.np >= 3 && feat == 0) feat = kFeatPlanes;
+    return feat;
+}
+
+// The fix-up variant serves the single-sample, ≤ 64-sphere, no-feature launches (C2) of frame
+// batches (kPkFixMinFrames frames or more) that neither count rays nor record tile costs.  A
+// one-frame launch keeps the marching variant: the fix-up launch's latency (its slowest pixel's
+// exact march, ~20 µs) would be added to every frame (C2 45 → 72 µs per single launch), while a
+// batch pays it once.  RTAMD_PK_FIX=0 keeps the marching variant everywhere (A/B).
+constexpr uint32_t kPkFixMinFrames = 8;
+bool packet_uses_fixup(const TraceParams& p, bool count, bool any_specular) {
+    const char* e = std::getenv("RTAMD_PK_FIX");  // read per launch (tests switch it)
+    const bool off = e && std::atoi(e) == 0;
+    return !off && !count && p.aa == 1 && !p.tile_cost && p.nframes >= kPkFixMinFrames &&
+           (p.ns + 63) / 64 <= 1 && packet_features(p, any_specular) == 0;
+}
+
+hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specular,
+                                hipStream_t stream) {
+    const size_t lds = packet_lds_bytes(p.ns, p.np, p.nl);
+    const int chunks = (p.ns + 63) / 64;
+    int feat = packet_features(p, any_specular);
+    if (packet_uses_fixup(p, count, any_specular)) {
+        if (!p.fix_list || !p.fix_ctl) return hipErrorInvalidValue;
+        feat = kFeatFix;
+    }
     // the area-light variants live in rt_packet_area.hip (compiled with the default scheduler)
     if (feat == kFeatArea) return launch_packet_area(p, count, lds, chunks, stream);
     if (chunks <= 1) launch_packet_maxc<1>(p, count, lds, feat, stream);

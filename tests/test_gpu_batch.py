@@ -472,3 +472,70 @@ def test_gather_all_batch_rejects_unequal_root_weights():
     finally:
         for c in ctxs:
             c.close()
+
+
+# ------------------------------------------------------------------ the fix-up variant (C2)
+@pytest.mark.parametrize("name,w,h,n", [("c2", 1920, 1080, 8), ("c2", 1920, 1080, 32),
+                                        ("c2", 480, 270, 9), ("c2", 97, 61, 12),
+                                        ("c2", 480, 270, 4)])  # below 8 frames: marching
+def test_fixup_variant_equals_marching_variant(ctx, monkeypatch, name, w, h, n):
+    """The fix-up variant of the packet kernel (C2's shape: single sample, <= 64 spheres, no
+    other feature) does not march undecided shadow rays; their pixels are queued and re-rendered
+    by packet_fixup_kernel with the exact per-pixel path (batches of 8 frames or more).  Every
+    frame (HDR, float3 and Reinhard bytes) equals the marching variant's (RTAMD_PK_FIX=0): moving
+    and repeated cameras, a row set of the multi-GPU split, an odd-sized frame (lanes past the
+    edge)."""
+    sc = make_config(name, w, h)
+    ds = ctx.scene(sc)
+    try:
+        pos = _positions(ds, n, seed=23)
+        for opts in (capi.default_opts(tonemap=1),
+                     capi.default_opts(tonemap=1, row_begin=16, row_end=h, row_block=16,
+                                       row_cycle=3)):
+            rows = capi.rendered_rows(opts, h)
+            outs = {}
+            for fix in ("1", "0"):
+                monkeypatch.setenv("RTAMD_PK_FIX", fix)
+                H64 = torch.full((n * rows * w * 3,), -1.0, dtype=torch.float64, device="cuda")
+                H32 = torch.full((n * rows * w * 3,), -1.0, dtype=torch.float32, device="cuda")
+                L8 = torch.zeros(n * rows * w * 3, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
+                ds.render_batch(ds.cameras(pos), H64.data_ptr(), H32.data_ptr(), L8.data_ptr(),
+                                opts)
+                ctx.synchronize()
+                outs[fix] = (H64.cpu().numpy(), H32.cpu().numpy(), L8.cpu().numpy())
+            for a, b in zip(outs["1"], outs["0"]):
+                assert np.array_equal(a, b)
+    finally:
+        ds.close()
+
+
+def test_fixup_variant_vs_oracle_on_undecided_shadows(ctx, oracle):
+    """A scene built to leave many shadow rays undecided (spheres resting on the floor and
+    touching each other, the light just above them): the fix-up variant's frame equals the C
+    oracle bit for bit."""
+    from raytracingengine_amd.scene import Camera, Material, SceneData
+    sc = SceneData(Camera((0.0, 0.0, -25.0), 160.0, 320, 180, 0.0, 200.0, 1), name="touching")
+    for i in range(8):
+        sc.add_sphere((-7.0 + 2.0 * i, -9.0, 3.0), 1.0, Material((0.8, 0.3 + 0.05 * i, 0.4)))
+        sc.add_sphere((-7.0 + 2.0 * i, -7.0, 3.0), 1.0, Material((0.3, 0.7, 0.2 + 0.05 * i)))
+    sc.add_plane((0.0, -10.0, 0.0), (0.0, 1.0, 0.0), Material((0.9, 0.9, 0.9)))
+    sc.add_plane((0.0, 0.0, 15.0), (0.0, 0.0, -1.0), Material((0.7, 0.8, 0.9)))
+    sc.add_light((0.3, -5.9, 3.0), (1.0, 1.0, 1.0), 40.0)
+    ds = ctx.scene(sc)
+    n = 8  # a batch: the fix-up variant
+    try:
+        H64 = torch.empty(n * 180 * 320 * 3, dtype=torch.float64, device="cuda")
+        L8 = torch.empty(n * 180 * 320 * 3, dtype=torch.uint8, device="cuda")
+        ds.render_batch(ds.cameras(np.repeat(ds.camera["position"], n, axis=0)), H64.data_ptr(),
+                        None, L8.data_ptr(), capi.default_opts(tonemap=1))
+        ctx.synchronize()
+        got64 = H64.cpu().numpy().reshape(n, 180, 320, 3)
+        got8 = L8.cpu().numpy().reshape(n, -1)
+    finally:
+        ds.close()
+    ref, _, _ = oracle.render(sc)
+    ref8 = oracle.tonemap(ref, 1).reshape(-1)
+    for f in range(n):
+        assert np.array_equal(got64[f], ref), f
+        assert np.array_equal(got8[f], ref8), f

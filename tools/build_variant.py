@@ -1,6 +1,7 @@
 """Dev tool: build an A/B (or ablation) library from a patched copy of one source.
 
     python tools/build_variant.py NAME FILE 'old text' 'new text' ['old' 'new' ...] [-D MACRO ...]
+        [--flags "extra hipcc flags replacing the source's in-tree extras"] [--src a.hip,b.hip]
 
 FILE is a source under raytracingengine_amd/csrc; the copy (with every replacement applied,
 each must match) is compiled with the in-tree flags and linked with the in-tree objects of the
@@ -16,6 +17,11 @@ srcs = None  # --src a.hip,b.hip: the sources to recompile (when FILE is a heade
 if "--src" in args:
     i = args.index("--src")
     srcs = args[i + 1].split(",")
+    del args[i:i + 2]
+extra = None  # --flags "...": replaces the in-tree per-source extra flags of the patched file(s)
+if "--flags" in args:
+    i = args.index("--flags")
+    extra = args[i + 1].split()
     del args[i:i + 2]
 defs = []
 while "-D" in args:
@@ -38,7 +44,8 @@ inc = f"-I{os.path.join(B.ROOT, 'include')}"
 rebuilt = {}
 for src in srcs or [fname]:
     obj = os.path.join(tmp, src + ".o")
-    r = subprocess.run([B.HIPCC, *B.HIP_FLAGS, *B.EXTRA_FLAGS.get(src, []), *defs, inc, "-c",
+    flags = B.EXTRA_FLAGS.get(src, []) if extra is None else extra
+    r = subprocess.run([B.HIPCC, *B.HIP_FLAGS, *flags, *defs, inc, "-c",
                         "-o", obj, os.path.join(src_dir, src)], stderr=subprocess.PIPE, text=True)
     if r.returncode:  # the errors only (the warnings of these sources are known)
         sys.exit("\n".join(l for l in r.stderr.splitlines() if "error" in l) or r.stderr[-4000:])
