@@ -1481,23 +1481,14 @@ hipError_t launch_packet_image_batch(const TraceParams& p, const PkImageJobs& jo
 // march (rt_trace_common.hpp trace_direct) — the same image bits as the packet kernel, stored
 // like it.  A persistent grid over the device-side count; its last workgroup zeroes the count
 // for the next launch (no memset on the stream).
+// The fix-up is latency-bound (about one wave per SIMD, each running a whole pixel), so the scene
+// records are staged into LDS when they fit (LDS instead of L2 latency in the sphere loops).
 constexpr int kFixThreads = 256;
+template <bool LDS>
 __global__ __launch_bounds__(kFixThreads) void packet_fixup_kernel(TraceParams P) {
+    extern __shared__ double smem[];
     const uint32_t n = __hip_atomic_load(P.fix_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    SceneView S;
-    S.ns = P.ns;
-    S.np = P.np;
-    S.nt = P.nt;
-    S.nl = P.nl;
-    S.sph = P.sph;
-    S.pl = P.pl;
-    S.lt = P.lt;
-    S.tri = P.tri;
-    S.sph_mat = P.sph_mat;
-    S.pl_mat = P.pl_mat;
-    S.tri_mat = P.tri_mat;
-    S.bvh = P.bvh;
-    S.bvh_tri = P.bvh_tri;
+    const SceneView S = stage_scene<LDS>(P, smem, threadIdx.x, kFixThreads);
     Counts cnt{0u, 0u};
     for (uint32_t i = blockIdx.x * kFixThreads + threadIdx.x; i < n; i += gridDim.x * kFixThreads) {
         const uint64_t o = P.fix_list[i];
@@ -1526,7 +1517,11 @@ __global__ __launch_bounds__(kFixThreads) void packet_fixup_kernel(TraceParams P
 
 hipError_t launch_packet_fixup(const TraceParams& p, hipStream_t stream) {
     if (!p.fix_list || !p.fix_ctl) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(packet_fixup_kernel, dim3(256), dim3(kFixThreads), 0, stream, p);
+    const size_t lds = sizeof(double) * scene_doubles(p);
+    if (lds <= 32 * 1024)
+        hipLaunchKernelGGL(packet_fixup_kernel<true>, dim3(256), dim3(kFixThreads), lds, stream, p);
+    else
+        hipLaunchKernelGGL(packet_fixup_kernel<false>, dim3(256), dim3(kFixThreads), 0, stream, p);
     return hipGetLastError();
 }
 
