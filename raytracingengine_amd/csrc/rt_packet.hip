@@ -1480,15 +1480,27 @@ hipError_t launch_packet_image_batch(const TraceParams& p, const PkImageJobs& jo
 // generic closest hit over every primitive, occlusion_opaque and the exact computeTransmittance
 // march (rt_trace_common.hpp trace_direct) — the same image bits as the packet kernel, stored
 // like it.  A persistent grid over the device-side count; its last workgroup zeroes the count
-// for the next launch (no memset on the stream).
-// The fix-up is latency-bound (about one wave per SIMD, each running a whole pixel), so the scene
-// records are staged into LDS when they fit (LDS instead of L2 latency in the sphere loops).
+// for the next launch (no memset on the stream).  The scene records are staged into LDS when
+// they fit.  Its cost is per wave, ~2 300 VALU + 1 100 SALU (~45k cycles) each: one wave per
+// 64 queued pixels is the fastest arrangement — 16, 8 or 4 pixels per wave (more waves per SIMD)
+// took 75 / 152 / 334 µs against 26 µs per 32-frame C2 batch, lanes of a group sharing one
+// pixel's sphere loops 42 µs, a per-ray capsule mask for the marches no change
+// (profiles/r05_ab_fixup.txt).
 constexpr int kFixThreads = 256;
+constexpr int kFixBlocks = 256;
 template <bool LDS>
 __global__ __launch_bounds__(kFixThreads) void packet_fixup_kernel(TraceParams P) {
     extern __shared__ double smem[];
     const uint32_t n = __hip_atomic_load(P.fix_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const SceneView S = stage_scene<LDS>(P, smem, threadIdx.x, kFixThreads);
+    // the fix-up variants' scenes: spheres, planes and point lights, no specular material, so
+    // no triangle, BVH, area-light or pow code is compiled in (229 -> 167 VGPRs, 288 -> 40 B of
+    // scratch: 27.5 -> 26 µs per 32-frame batch)
+    SceneView S = stage_scene<LDS>(P, smem, threadIdx.x, kFixThreads);
+    S.nt = 0;
+    S.al = 0;
+    S.spec = false;
+    S.tri = S.tri_mat = S.bvh = nullptr;
+    S.bvh_tri = nullptr;
     Counts cnt{0u, 0u};
     for (uint32_t i = blockIdx.x * kFixThreads + threadIdx.x; i < n; i += gridDim.x * kFixThreads) {
         const uint64_t o = P.fix_list[i];
@@ -1517,11 +1529,14 @@ __global__ __launch_bounds__(kFixThreads) void packet_fixup_kernel(TraceParams P
 
 hipError_t launch_packet_fixup(const TraceParams& p, hipStream_t stream) {
     if (!p.fix_list || !p.fix_ctl) return hipErrorInvalidValue;
+    if (p.nt != 0 || p.al_samples != 0) return hipErrorInvalidValue;  // the lean scene view
     const size_t lds = sizeof(double) * scene_doubles(p);
     if (lds <= 32 * 1024)
-        hipLaunchKernelGGL(packet_fixup_kernel<true>, dim3(256), dim3(kFixThreads), lds, stream, p);
+        hipLaunchKernelGGL(packet_fixup_kernel<true>, dim3(kFixBlocks), dim3(kFixThreads), lds,
+                           stream, p);
     else
-        hipLaunchKernelGGL(packet_fixup_kernel<false>, dim3(256), dim3(kFixThreads), 0, stream, p);
+        hipLaunchKernelGGL(packet_fixup_kernel<false>, dim3(kFixBlocks), dim3(kFixThreads), 0,
+                           stream, p);
     return hipGetLastError();
 }
 

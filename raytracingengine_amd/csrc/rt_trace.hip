@@ -196,6 +196,8 @@ __device__ __forceinline__ SceneView global_view(const TraceParams& P) {
     S.np = P.np;
     S.nt = P.nt;
     S.nl = P.nl;
+    S.al = P.al_samples;
+    S.spec = true;
     S.sph = P.sph;
     S.pl = P.pl;
     S.lt = P.lt;

@@ -62,6 +62,8 @@ struct SceneView {
     const double* bvh;       // triangle BVH (null: every triangle is tested)
     const int32_t* bvh_tri;
     int ns, np, nt, nl;
+    int al;  // samples of the build-defined area light (TraceParams.al_samples), 0: none
+    bool spec;  // false: no material has specular > 0 (the Blinn-Phong term is not compiled in)
 };
 
 struct Hit {
@@ -280,6 +282,8 @@ __device__ __forceinline__ SceneView stage_scene(const TraceParams& P, double* s
     S.np = P.np;
     S.nt = P.nt;
     S.nl = P.nl;
+    S.al = P.al_samples;
+    S.spec = true;
     S.tri = P.tri;
     S.sph_mat = P.sph_mat;
     S.pl_mat = P.pl_mat;
@@ -555,7 +559,7 @@ __device__ __forceinline__ void light_term(const SceneView& S, d3 P, d3 n, d3 vi
     }
     if (T <= bias) return;
     diff = diff + ((E * inv_d2) * ndl) * T;
-    if (m[5] <= 0.0 && m[4] > 0.0) {  // transparency, specular
+    if (S.spec && m[5] <= 0.0 && m[4] > 0.0) {  // transparency, specular
         const d3 H = unit(L + view);
         const double ndh = smax(0.0, dot(n, H));
         if (ndh > 0.0) {
@@ -589,7 +593,7 @@ __device__ __forceinline__ void light_term_wave(const SceneView& S, bool active,
                                : transmittance_t<true>(S, so, L, dist - bias, bias, mask);
     if (T <= bias) return;
     diff = diff + ((E * inv_d2) * ndl) * T;
-    if (m[5] <= 0.0 && m[4] > 0.0) {  // transparency, specular
+    if (S.spec && m[5] <= 0.0 && m[4] > 0.0) {  // transparency, specular
         const d3 H = unit(L + view);
         const double ndh = smax(0.0, dot(n, H));
         if (ndh > 0.0) {
@@ -613,14 +617,14 @@ __device__ __forceinline__ d3 direct(const SceneView& S, const TraceParams& P, d
                           diff, spec, cnt);
     }
 #ifndef RT_LEAN_GENERIC  // ... and without the area light
-    if (P.al_samples > 0) {
+    if (S.al > 0) {
         const uint32_t stream = 0x10000u + (sample << 6) + static_cast<uint32_t>(depth);
         const double k = static_cast<double>(P.al_k);
         const d3 corner = mk(P.al_corner[0], P.al_corner[1], P.al_corner[2]);
         const d3 eu = mk(P.al_u[0], P.al_u[1], P.al_u[2]);
         const d3 ev = mk(P.al_v[0], P.al_v[1], P.al_v[2]);
         const d3 E = mk(P.al_E[0], P.al_E[1], P.al_E[2]);
-        for (int s = 0; s < P.al_samples; ++s) {
+        for (int s = 0; s < S.al; ++s) {
             const double r1 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(s));
             const double r2 = u01(P.seed, pix, stream, 2u * static_cast<uint32_t>(s) + 1u);
             const double fu = (static_cast<double>(s % P.al_k) + r1) / k;
