@@ -39,6 +39,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
@@ -329,7 +331,9 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     rt_render_gather_batch call: this rank's rows of the HDR framebuffer stay on the rank, the
     fused bytes are gathered to rank 0 (one gather per batch; none at N=1) and assembled.
     gather=False: every rank renders whole frames of its own (weak scaling; same call on a
-    one-rank view).  camera_step(base, frame) -> a new camera position per frame.
+    one-rank view).  camera_step(base, frames) -> a new camera position per frame ([n, 3], one
+    vectorised call per batch: the positions of the batch that opens the timed region are formed
+    inside it, before its launch, while the GPU waits).
     weight > 1: rank 0 renders `weight` of the weight + N − 1 row sets (rt_comm_set_root_weight)."""
     torch, capi = R.torch, R.capi
     W, H = sc.camera.width, sc.camera.height
@@ -377,7 +381,7 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     def cams_for(f0, n):
         if camera_step is None:
             return static_cams[:n]
-        return dscene.cameras([camera_step(base, f0 + j) for j in range(n)])
+        return dscene.cameras(camera_step(base, np.arange(f0, f0 + n)))
 
     def step(f0, n, timed):
         b = nb[0]
@@ -667,7 +671,7 @@ def main(argv=None):
                 "value": round(f32["rays"] * steps_x / f32["elapsed"] / 1e6, 3)}
             mv = split_frames(R, sc, steps_x, args.warmup, batch, args.hdr, tonemap,
                               event_every=args.event_every,
-                              camera_step=lambda base, i: base + (i * 1e-7, 0.0, 0.0))
+                              camera_step=lambda base, i: base + np.outer(i * 1e-7, (1, 0, 0)))
             line["moving_camera"] = {
                 "ms_per_step": round(mv["elapsed"] / steps_x * 1e3, 5),
                 "kernel_ms_per_frame": round(kernel_ms_per_frame(mv, args.event_every), 6),

@@ -320,6 +320,18 @@ rt_status tile_order(rt_context* ctx, rt_scene::PkImage& im, TraceParams& p, int
     return RT_OK;
 }
 
+// A launch whose camera has no image entry yet (a moving camera): an order built earlier for the
+// same launch shape under another camera of the scene, if any — an order only permutes which
+// workgroup renders which tile, and nearby cameras share their costly tiles.
+rt_status scene_tile_order(rt_context* ctx, const rt_scene* sc, TraceParams& p, int flags,
+                           rt_scene::PkImage::TileOrder** rec) {
+    for (auto& im : sc->pk_images) {
+        const rt_status st = tile_order(ctx, im, p, flags, rec, true);
+        if (st != RT_OK || p.tile_order) return st;
+    }
+    return RT_OK;
+}
+
 // The cached image of this camera position, or null; a render on another stream than the one
 // that formed it waits for the entry's event until it has completed.
 rt_status packet_image_cached(rt_context* ctx, const rt_scene* sc, const double* cam,
@@ -392,7 +404,10 @@ rt_status packet_image(rt_context* ctx, const rt_scene* sc, TraceParams& p, int 
         p.pk_image = static_cast<const double*>(found->buf.ptr);
         return tile_order(ctx, *found, p, flags, rec);
     }
-    if (!packet_second_sighting(sc, p.cam_pos)) return packet_publish_slot(ctx, sc, p);
+    if (!packet_second_sighting(sc, p.cam_pos)) {
+        const rt_status st2 = packet_publish_slot(ctx, sc, p);
+        return st2 != RT_OK ? st2 : scene_tile_order(ctx, sc, p, flags, rec);
+    }
     rt_scene::PkImage* im = nullptr;
     st = packet_image_entry(ctx, sc, p.cam_pos, p, &im);
     if (st != RT_OK) return st;
@@ -501,7 +516,7 @@ rt_status packet_batch_images(rt_context* ctx, const rt_scene* sc, const rt_came
         return hip_fail(e, "packet batch images");
     }
     if (kind[0] == kCached) return tile_order(ctx, *ent[0], p, flags, rec, !same_cam);
-    return RT_OK;
+    return scene_tile_order(ctx, sc, p, flags, rec);
 }
 
 // Whether a render of this TraceRay shape takes the breadth-first path, whose arena (ctx->wf,
