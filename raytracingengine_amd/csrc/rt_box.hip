@@ -40,6 +40,18 @@ namespace rtamd {
 #define RT_BOX_MULTI_WAVES 3
 #endif
 
+// The SPH instantiations (mirror) read the hit's material at each use and park its normal and
+// incident direction in LDS across the light loop, for the reflection ray: 112 -> 32 B/lane of
+// scratch at 4 waves/SIMD, mirror 1.326 -> 1.231 ms (profiles/r05_ab_box_spheres.txt; the hit
+// point and shading normal parked as well: 1.239 ms).  The planes-only ones keep both in
+// registers (reading the material at use: C1 +1.6 %, at AA = 32 +2.7 %).  RT_BOX_PARK=0: A/B.
+#ifndef RT_BOX_PARK
+#define RT_BOX_PARK 1
+#endif
+constexpr bool kBoxPark = RT_BOX_PARK != 0;
+constexpr int kBoxParkStride = 256;  // threads per workgroup of both box kernels
+constexpr int kBoxParkSlots = 6;
+
 // wave-uniform reads through the scalar data cache
 typedef const __attribute__((address_space(4))) double* cdp;
 
@@ -52,6 +64,7 @@ struct BoxScene {
     const double* mat;    // material table [spheres | planes] (per-lane reads)
     int n[4];         // planes per group: normal ±e_x, ±e_y, ±e_z, any other
     int nl, ns;
+    double* park;     // kBoxPark: this thread's LDS slots (stride kBoxParkStride)
 };
 
 struct BoxHit {
@@ -351,14 +364,32 @@ __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& 
         gn = mk(r[3], r[4], r[5]);  // Plane::GetNormalAt (Shape.h:161-163)
         unit_n = r[7] != 0.0;       // |n| rounds to exactly 1: normalize() returns n
     }
-    const Mat m = load_mat(box_material(S, h));
+    // the material record (r g b shininess specular transparency ior): SPH reads it at each use
+    // (a copy of its seven values stayed live across the light loop: 14 VGPRs), the planes-only
+    // instantiations keep the copy
+    const double* mp = box_material(S, h);
+    double mc[7];
+    if constexpr (!SPH)
+        for (int k = 0; k < 7; ++k) mc[k] = mp[k];
+    auto mat = [&](int k) -> double {
+        if constexpr (SPH) return mp[k];
+        else return mc[k];
+    };
     const d3 inc = unit(d);
     const bool front = dot(gn, inc) < 0.0;
     const d3 n0 = front ? gn : -gn;
     const d3 view = -inc;
-    const double tr = sclamp(m.transparency, 0.0, 1.0);
     // directLightning (Scene.h:79-129)
     const d3 n = unit_n ? n0 : unit(n0);
+    if constexpr (SPH && kBoxPark) {  // n0 and inc wait in LDS for the reflection ray
+        S.park[0 * kBoxParkStride] = n0.x;
+        S.park[1 * kBoxParkStride] = n0.y;
+        S.park[2 * kBoxParkStride] = n0.z;
+        S.park[3 * kBoxParkStride] = inc.x;
+        S.park[4 * kBoxParkStride] = inc.y;
+        S.park[5 * kBoxParkStride] = inc.z;
+        __asm__ volatile("" ::: "memory");
+    }
     d3 diff = mk(0.0, 0.0, 0.0), spec = mk(0.0, 0.0, 0.0);
     for (int i = 0; i < S.nl; ++i) {
         cdp l = S.lt + kLtStride * i;
@@ -377,25 +408,38 @@ __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& 
                                   : box_transmittance<SPH>(S, so, L, dist - bias, bias);
         if (T <= bias) continue;
         diff = diff + ((E * inv_d2) * ndl) * T;
-        if (m.transparency <= 0.0 && m.specular > 0.0) {
-            const d3 H = unit(L + view);
+        if (mat(5) <= 0.0 && mat(4) > 0.0) {
+            d3 vw = view;
+            if constexpr (SPH && kBoxPark)
+                vw = -mk(S.park[3 * kBoxParkStride], S.park[4 * kBoxParkStride],
+                         S.park[5 * kBoxParkStride]);
+            const d3 H = unit(L + vw);
             const double ndh = smax(0.0, dot(n, H));
             if (ndh > 0.0) {
-                const double sf = pow_bp_t<true>(ndh, m.shininess);
+                const double sf = pow_bp_t<true>(ndh, mat(3));
                 spec = spec + ((E * inv_d2) * sf) * T;
             }
         }
     }
-    const d3 local = hmul(m.color, diff) + spec * m.specular;
+    const d3 local = hmul(mk(mat(0), mat(1), mat(2)), diff) + spec * mat(4);
+    const double tr = sclamp(mat(5), 0.0, 1.0);
     d3 fin = mk(0.0, 0.0, 0.0);
     if (tr < 1.0) fin = fin + local * (1.0 - tr);
     nd.value = fin;
-    if (m.specular > bias) {
-        const d3 R = unit(reflect(inc, n0));
+    if (mat(4) > bias) {
+        d3 inc_c = inc, n0_c = n0;
+        if constexpr (SPH && kBoxPark) {
+            __asm__ volatile("" ::: "memory");
+            n0_c = mk(S.park[0 * kBoxParkStride], S.park[1 * kBoxParkStride],
+                      S.park[2 * kBoxParkStride]);
+            inc_c = mk(S.park[3 * kBoxParkStride], S.park[4 * kBoxParkStride],
+                       S.park[5 * kBoxParkStride]);
+        }
+        const d3 R = unit(reflect(inc_c, n0_c));
         nd.refl = true;
         nd.rd = R;
         nd.ro = hp + R * bias;
-        nd.rw = m.specular;
+        nd.rw = mat(4);
     }
     return nd;
 }
@@ -435,6 +479,7 @@ __device__ __forceinline__ BoxScene box_scene(const TraceParams& P) {
     for (int k = 0; k < 4; ++k) S.n[k] = P.box ? P.box_n[k] : 0;
     S.nl = P.nl;
     S.ns = P.ns;
+    S.park = nullptr;
     return S;
 }
 
@@ -470,7 +515,11 @@ __global__ __launch_bounds__(kBoxAaThreads, RT_BOX_WAVES) void box_aa_kernel(Tra
     const uint64_t npx = static_cast<uint64_t>(P.width) * P.rows;
     const uint64_t lin = static_cast<uint64_t>(blockIdx.x) * ppw + pl;
     Counts cnt{0u, 0u};
-    const BoxScene S = box_scene(P);
+    BoxScene S = box_scene(P);
+    if constexpr (SPH && kBoxPark) {
+        __shared__ double s_park[kBoxParkSlots * kBoxParkStride];
+        S.park = s_park + tid;
+    }
     if (pl < ppw && lin < npx) {
         const uint32_t x = static_cast<uint32_t>(lin % P.width);
         const uint32_t y = image_row(P, static_cast<uint32_t>(lin / P.width));
@@ -501,7 +550,11 @@ __global__ __launch_bounds__(kTileW * kTileH, SINGLE ? RT_BOX_WAVES : RT_BOX_MUL
     const uint32_t x = blockIdx.x * kTileW + threadIdx.x;
     const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
     Counts cnt{0u, 0u};
-    const BoxScene S = box_scene(P);
+    BoxScene S = box_scene(P);
+    if constexpr (SPH && kBoxPark) {
+        __shared__ double s_park[kBoxParkSlots * kBoxParkStride];
+        S.park = s_park + threadIdx.y * kTileW + threadIdx.x;
+    }
     if (x < P.width && yl < P.rows) {
         const uint32_t y = image_row(P, yl);
         const uint64_t pix = static_cast<uint64_t>(y) * P.width + x;
