@@ -1499,7 +1499,6 @@ __global__ __launch_bounds__(kFixThreads) void packet_fixup_kernel(TraceParams P
     S.nt = 0;
     S.al = 0;
     S.spec = false;
-    S.fast_roots = true;
     S.tri = S.tri_mat = S.bvh = nullptr;
     S.bvh_tri = nullptr;
     Counts cnt{0u, 0u};

@@ -198,7 +198,6 @@ __device__ __forceinline__ SceneView global_view(const TraceParams& P) {
     S.nl = P.nl;
     S.al = P.al_samples;
     S.spec = true;
-    S.fast_roots = false;
     S.sph = P.sph;
     S.pl = P.pl;
     S.lt = P.lt;

@@ -64,10 +64,6 @@ struct SceneView {
     int ns, np, nt, nl;
     int al;  // samples of the build-defined area light (TraceParams.al_samples), 0: none
     bool spec;  // false: no material has specular > 0 (the Blinn-Phong term is not compiled in)
-    // true (packet_fixup_kernel, latency-bound): the sphere roots through the sqrt / division
-    // cores with one refined reciprocal of 2a per ray (the packet kernel's sphere_roots_core:
-    // the same bits) instead of IEEE sqrt and two divisions per sphere
-    bool fast_roots;
 };
 
 struct Hit {
@@ -199,9 +195,6 @@ __device__ __forceinline__ bool closest_t(const SceneView& S, d3 o, d3 d, Hit& h
     const double a = dot(d, d);       // Shape.h:75 (same value for every sphere)
     const double two_a = 2.0 * a;     // Shape.h:85-86 denominator
     const double four_a = 4.0 * a;    // Shape.h:79: (4.0 * a) * c
-    // fast_roots: 2a in [2^-100, 2^100] gives t0 <= t1 and a refined reciprocal in range
-    const bool fast = S.fast_roots && two_a >= 0x1p-100 && two_a <= 0x1p100;
-    const double r2a = fast ? rcp_refined(two_a) : 0.0;
     for (int j = 0; MASKED ? mask != 0ull : j < S.ns; ++j) {
         int i = j;
         if constexpr (MASKED) {
@@ -214,30 +207,18 @@ __device__ __forceinline__ bool closest_t(const SceneView& S, d3 o, d3 d, Hit& h
         const double c = dot(oc, oc) - s[3];
         const double disc = b * b - four_a * c;
         if (disc < 0.0) continue;
-        double t;
-        if (fast && disc >= 0x1p-767 && disc <= 0x1.fffffffffffffp+1023) {
-            // rt_packet.hip sphere_roots_core: a numerator |n| >= 2^-900 divides exactly, a
-            // smaller one gives |t| < 2^-790 both ways, so the 1e-6 tests decide alike
-            const double sq = sqrt_core(disc);
-            t = div_core(-b - sq, two_a, r2a);
-            if (t < 1e-6) {
-                t = div_core(-b + sq, two_a, r2a);
-                if (t < 1e-6) continue;
-            }
-        } else {
-            const double sq = sqrt(disc);
-            double t0 = (-b - sq) / two_a;
-            double t1 = (-b + sq) / two_a;
-            if (t0 > t1) {
-                const double tmp = t0;
-                t0 = t1;
-                t1 = tmp;
-            }
-            t = t0;
-            if (t < 1e-6) {
-                t = t1;
-                if (t < 1e-6) continue;
-            }
+        const double sq = sqrt(disc);
+        double t0 = (-b - sq) / two_a;
+        double t1 = (-b + sq) / two_a;
+        if (t0 > t1) {
+            const double tmp = t0;
+            t0 = t1;
+            t1 = tmp;
+        }
+        double t = t0;
+        if (t < 1e-6) {
+            t = t1;
+            if (t < 1e-6) continue;
         }
         if (!found || t < best) {
             found = true;
@@ -303,7 +284,6 @@ __device__ __forceinline__ SceneView stage_scene(const TraceParams& P, double* s
     S.nl = P.nl;
     S.al = P.al_samples;
     S.spec = true;
-    S.fast_roots = false;
     S.tri = P.tri;
     S.sph_mat = P.sph_mat;
     S.pl_mat = P.pl_mat;
