@@ -610,6 +610,10 @@ def main(argv=None):
             "frames_per_call": batch, "rays_per_frame": int(res["rays"]),
         },
         "frames_per_sec": round(args.steps / elapsed, 3),
+        # the library this run loaded: the sources it was compiled from (rt_build_info) and
+        # whether they are the sources of this tree
+        "build": {k: v for k, v in capi.build_info().items() if k in
+                  ("source_sha256", "matches_tree", "arch", "hipcc")},
         "root_weight_probe": probe,
         "clock_warmup_ms": args.clock_warmup_ms,
         "kernel_ms_per_frame": round(render_ms, 6),

@@ -188,6 +188,12 @@ typedef struct rt_scene rt_scene;
 /* Thread-local message of the most recent failure ("" if none). */
 const char* rt_last_error(void);
 
+/* The build record of this library (no reference counterpart): a static JSON object with the
+ * sha256 of the sources, headers and flags it was compiled from ("source_sha256"), the target
+ * ("arch") and the compiler ("hipcc"), so that a run can check which sources its binary holds
+ * (raytracingengine_amd/build.py source_digest). */
+const char* rt_build_info(void);
+
 /* Number of visible HIP devices (0 when none). */
 int rt_device_count(void);
 

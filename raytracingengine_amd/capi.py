@@ -37,7 +37,7 @@ RT_COMM_ID_BYTES = 128
 
 # Every symbol include/rt_capi.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED = [
-    "rt_last_error", "rt_device_count", "rt_render_opts_default", "rt_context_create",
+    "rt_last_error", "rt_build_info", "rt_device_count", "rt_render_opts_default", "rt_context_create",
     "rt_context_destroy", "rt_context_set_stream", "rt_context_synchronize", "rt_scene_create",
     "rt_scene_destroy", "rt_scene_set_area_light", "rt_render", "rt_render_device",
     "rt_render_multi", "rt_comm_unique_id", "rt_comm_create", "rt_comm_create_all",
@@ -111,6 +111,9 @@ def load_library(path: str = LIB_PATH):
     L = ctypes.CDLL(path)
     vp, i32 = ctypes.c_void_p, ctypes.c_int
     L.rt_last_error.restype = ctypes.c_char_p
+    if hasattr(L, "rt_build_info") or "RTAMD_LIB" not in os.environ:
+        L.rt_build_info.restype = ctypes.c_char_p
+        L.rt_build_info.argtypes = []
     L.rt_device_count.restype = i32
     L.rt_render_opts_default.argtypes = [vp]
     L.rt_render_opts_default.restype = None
@@ -167,6 +170,17 @@ def load_library(path: str = LIB_PATH):
         fn.restype = i32
     _lib = L
     return L
+
+
+def build_info() -> dict:
+    """The loaded library's build record (rt_build_info), plus `matches_tree`: whether its
+    source_sha256 equals the digest of the sources in this tree (raytracingengine_amd/build.py
+    source_digest) — False means the binary is stale against its sources."""
+    import json
+    info = json.loads(load_library().rt_build_info().decode())
+    from . import build
+    info["matches_tree"] = info.get("source_sha256") == build.source_digest()
+    return info
 
 
 def _check(status: int):

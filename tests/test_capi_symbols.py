@@ -48,6 +48,15 @@ def test_library_is_gfx950_only():
     assert set(re.findall(rb"gfx[0-9]{3,4}[a-z]?", blob)) == {b"gfx950"}
 
 
+def test_build_record_matches_tree(lib):
+    """rt_build_info names the sources the binary was compiled from: a stale librtamd.so (sources
+    edited after the build) shows as matches_tree False, here and in every bench line."""
+    info = capi.build_info()
+    assert info["arch"] == "gfx950"
+    assert len(info["source_sha256"]) == 64
+    assert info["matches_tree"], info
+
+
 def test_defaults_match_reference(lib):
     o = capi.default_opts()
     assert o.max_recursion == 10      # Scene.h:24

@@ -1025,3 +1025,12 @@ def test_box_spheres_equal_generic_chain(ctx, kind, aa, max_rec):
         loop = _render(ctx, sc, hdr64=True, tonemap=6, max_recursion=max_rec,
                        flags=capi.RT_FLAG_NO_SAMPLE_PARALLEL)
         assert np.array_equal(out["hdr64"], loop["hdr64"], equal_nan=True)
+
+
+def test_loaded_library_is_built_from_this_tree(ctx):
+    """The librtamd.so this GPU run loaded was compiled from exactly the sources in this tree
+    (rt_build_info's source_sha256 against build.source_digest), so the parity results above
+    belong to these sources, not to a stale binary."""
+    info = capi.build_info()
+    assert info["arch"] == "gfx950"
+    assert info["matches_tree"], info
