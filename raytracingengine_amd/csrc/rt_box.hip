@@ -148,6 +148,7 @@ __device__ __forceinline__ void box_spheres_closest(const BoxScene& S, d3 o, d3 
     const double a = dot(d, d);       // Shape.h:75 (same value for every sphere)
     const double two_a = 2.0 * a;     // Shape.h:85-86 denominator
     const double four_a = 4.0 * a;    // Shape.h:79: (4.0 * a) * c
+#pragma unroll 2  // mirror 1.227 -> 1.222 ms, at AA = 4 4.607 -> 4.572 ms
     for (int i = 0; i < S.ns; ++i) {
         cdp s = S.sph + kSphStride * i;
         const d3 oc = o - mk(s[0], s[1], s[2]);
