@@ -1708,16 +1708,22 @@ static int packet_features(const TraceParams& p, bool any_specular) {
 }
 
 // The fix-up variant serves the single-sample, ≤ 64-sphere, no-feature launches (C2) of frame
-// batches (kPkFixMinFrames frames or more) that neither count rays nor record tile costs.  A
-// one-frame launch keeps the marching variant: the fix-up launch's latency (its slowest pixel's
-// exact march, ~20 µs) would be added to every frame (C2 45 → 72 µs per single launch), while a
-// batch pays it once.  RTAMD_PK_FIX=0 keeps the marching variant everywhere (A/B).
-constexpr uint32_t kPkFixMinFrames = 8;
+// batches that neither count rays nor record tile costs, when the launch is large enough to pay
+// for its fix-up launch: that launch costs ~25 µs whatever it holds (one wave's serial generic
+// pixel), the march-free packet kernel saves ~1 ns per pixel (C2: 37.8 → 35.7 µs per 1080p
+// frame), so the break-even is ~25 M pixels per launch — kPkFixMinPixels (≈ 15 1080p frames)
+// leaves a margin: a 32-frame batch takes it, an 8-frame one or one rank's rows of a 4- or
+// 8-rank split keep the marching variant (profiles/r05_ab_fixup.txt).  RTAMD_PK_FIX=0: the
+// marching variant everywhere, =1: the fix-up variant for every eligible batch (tests, A/B).
+constexpr uint64_t kPkFixMinPixels = 32ull << 20;
 bool packet_uses_fixup(const TraceParams& p, bool count, bool any_specular) {
     const char* e = std::getenv("RTAMD_PK_FIX");  // read per launch (tests switch it)
-    const bool off = e && std::atoi(e) == 0;
-    return !off && !count && p.aa == 1 && !p.tile_cost && p.nframes >= kPkFixMinFrames &&
-           (p.ns + 63) / 64 <= 1 && packet_features(p, any_specular) == 0;
+    const int mode = e ? std::atoi(e) : -1;
+    if (mode == 0) return false;
+    const bool eligible = !count && p.aa == 1 && !p.tile_cost && p.nframes >= 1 &&
+                          (p.ns + 63) / 64 <= 1 && packet_features(p, any_specular) == 0;
+    const uint64_t px = static_cast<uint64_t>(p.nframes) * p.rows * p.width;
+    return eligible && (mode == 1 || px >= kPkFixMinPixels);
 }
 
 hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specular,

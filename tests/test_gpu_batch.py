@@ -477,11 +477,12 @@ def test_gather_all_batch_rejects_unequal_root_weights():
 # ------------------------------------------------------------------ the fix-up variant (C2)
 @pytest.mark.parametrize("name,w,h,n", [("c2", 1920, 1080, 8), ("c2", 1920, 1080, 32),
                                         ("c2", 480, 270, 9), ("c2", 97, 61, 12),
-                                        ("c2", 480, 270, 4)])  # below 8 frames: marching
+                                        ("c2", 480, 270, 4)])
 def test_fixup_variant_equals_marching_variant(ctx, monkeypatch, name, w, h, n):
     """The fix-up variant of the packet kernel (C2's shape: single sample, <= 64 spheres, no
     other feature) does not march undecided shadow rays; their pixels are queued and re-rendered
-    by packet_fixup_kernel with the exact per-pixel path (batches of 8 frames or more).  Every
+    by packet_fixup_kernel with the exact per-pixel path (batches of >= 32 M pixels, or any batch
+    with RTAMD_PK_FIX=1 as here).  Every
     frame (HDR, float3 and Reinhard bytes) equals the marching variant's (RTAMD_PK_FIX=0): moving
     and repeated cameras, a row set of the multi-GPU split, an odd-sized frame (lanes past the
     edge)."""
@@ -510,10 +511,11 @@ def test_fixup_variant_equals_marching_variant(ctx, monkeypatch, name, w, h, n):
         ds.close()
 
 
-def test_fixup_variant_vs_oracle_on_undecided_shadows(ctx, oracle):
+def test_fixup_variant_vs_oracle_on_undecided_shadows(ctx, oracle, monkeypatch):
     """A scene built to leave many shadow rays undecided (spheres resting on the floor and
     touching each other, the light just above them): the fix-up variant's frame equals the C
     oracle bit for bit."""
+    monkeypatch.setenv("RTAMD_PK_FIX", "1")  # the fix-up variant at this small size
     from raytracingengine_amd.scene import Camera, Material, SceneData
     sc = SceneData(Camera((0.0, 0.0, -25.0), 160.0, 320, 180, 0.0, 200.0, 1), name="touching")
     for i in range(8):
@@ -523,7 +525,7 @@ def test_fixup_variant_vs_oracle_on_undecided_shadows(ctx, oracle):
     sc.add_plane((0.0, 0.0, 15.0), (0.0, 0.0, -1.0), Material((0.7, 0.8, 0.9)))
     sc.add_light((0.3, -5.9, 3.0), (1.0, 1.0, 1.0), 40.0)
     ds = ctx.scene(sc)
-    n = 8  # a batch: the fix-up variant
+    n = 8  # a batch
     try:
         H64 = torch.empty(n * 180 * 320 * 3, dtype=torch.float64, device="cuda")
         L8 = torch.empty(n * 180 * 320 * 3, dtype=torch.uint8, device="cuda")
