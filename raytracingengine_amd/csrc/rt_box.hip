@@ -40,11 +40,12 @@ namespace rtamd {
 #define RT_BOX_MULTI_WAVES 3
 #endif
 
-// The SPH instantiations (mirror) read the hit's material at each use and park its normal and
-// incident direction in LDS across the light loop, for the reflection ray: 112 -> 32 B/lane of
-// scratch at 4 waves/SIMD, mirror 1.326 -> 1.231 ms (profiles/r05_ab_box_spheres.txt; the hit
-// point and shading normal parked as well: 1.239 ms).  The planes-only ones keep both in
-// registers (reading the material at use: C1 +1.6 %, at AA = 32 +2.7 %).  RT_BOX_PARK=0: A/B.
+// The hit's normal and incident direction wait in LDS across the light loop, for the reflection
+// ray, and the SPH instantiations (mirror) also read the hit's material at each use: 112 -> 32
+// B/lane of scratch at 4 waves/SIMD, mirror 1.326 -> 1.231 ms (profiles/r05_ab_box_spheres.txt;
+// the hit point and shading normal parked as well: 1.239 ms).  The planes-only ones keep the
+// material in registers (read at use: C1 +1.6 %, at AA = 32 +2.7 %); their park alone: C1 374 ->
+// 368.5 µs.  RT_BOX_PARK=0: A/B.
 #ifndef RT_BOX_PARK
 #define RT_BOX_PARK 1
 #endif
@@ -382,7 +383,7 @@ __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& 
     const d3 view = -inc;
     // directLightning (Scene.h:79-129)
     const d3 n = unit_n ? n0 : unit(n0);
-    if constexpr (SPH && kBoxPark) {  // n0 and inc wait in LDS for the reflection ray
+    if constexpr (kBoxPark) {  // n0 and inc wait in LDS for the reflection ray
         S.park[0 * kBoxParkStride] = n0.x;
         S.park[1 * kBoxParkStride] = n0.y;
         S.park[2 * kBoxParkStride] = n0.z;
@@ -411,7 +412,7 @@ __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& 
         diff = diff + ((E * inv_d2) * ndl) * T;
         if (mat(5) <= 0.0 && mat(4) > 0.0) {
             d3 vw = view;
-            if constexpr (SPH && kBoxPark)
+            if constexpr (kBoxPark)
                 vw = -mk(S.park[3 * kBoxParkStride], S.park[4 * kBoxParkStride],
                          S.park[5 * kBoxParkStride]);
             const d3 H = unit(L + vw);
@@ -429,7 +430,7 @@ __device__ __forceinline__ Node box_shade(const BoxScene& S, const TraceParams& 
     nd.value = fin;
     if (mat(4) > bias) {
         d3 inc_c = inc, n0_c = n0;
-        if constexpr (SPH && kBoxPark) {
+        if constexpr (kBoxPark) {
             __asm__ volatile("" ::: "memory");
             n0_c = mk(S.park[0 * kBoxParkStride], S.park[1 * kBoxParkStride],
                       S.park[2 * kBoxParkStride]);
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(kBoxAaThreads, RT_BOX_WAVES) void box_aa_kernel(Tra
     const uint64_t lin = static_cast<uint64_t>(blockIdx.x) * ppw + pl;
     Counts cnt{0u, 0u};
     BoxScene S = box_scene(P);
-    if constexpr (SPH && kBoxPark) {
+    if constexpr (kBoxPark) {
         __shared__ double s_park[kBoxParkSlots * kBoxParkStride];
         S.park = s_park + tid;
     }
@@ -552,7 +553,7 @@ __global__ __launch_bounds__(kTileW * kTileH, SINGLE ? RT_BOX_WAVES : RT_BOX_MUL
     const uint32_t yl = blockIdx.y * kTileH + threadIdx.y;
     Counts cnt{0u, 0u};
     BoxScene S = box_scene(P);
-    if constexpr (SPH && kBoxPark) {
+    if constexpr (kBoxPark) {
         __shared__ double s_park[kBoxParkSlots * kBoxParkStride];
         S.park = s_park + threadIdx.y * kTileW + threadIdx.x;
     }

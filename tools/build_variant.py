@@ -51,6 +51,7 @@ for src in srcs or [fname]:
         sys.exit("\n".join(l for l in r.stderr.splitlines() if "error" in l) or r.stderr[-4000:])
     rebuilt[src] = obj
 objs = [rebuilt.get(s, os.path.join(B.OBJ_DIR, s + ".o")) for s in B.SOURCES]
+objs.append(os.path.join(B.OBJ_DIR, "rt_build_info.cpp.o"))  # the in-tree build record
 out_dir = os.path.join(B.ROOT, "tools", "variants")
 os.makedirs(out_dir, exist_ok=True)
 out = os.path.join(out_dir, name + ".so")
