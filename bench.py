@@ -98,6 +98,38 @@ def load_profile(name: str):
         return json.load(fh), os.path.relpath(path, HERE)
 
 
+def launcher_command(args_list, gpus: int, port: int):
+    """The one child that runs `--gpus N > 1` when no outer launcher set WORLD_SIZE: N ranks of
+    this same script under torch.distributed.run (one process per GPU, rendezvous on
+    127.0.0.1), with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__), *args_list]
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """`python bench.py --gpus N` (N > 1) run plainly: start the N ranks as ONE child process
+    (torch.distributed.run), before this process makes any GPU call and without exec — rank 0's
+    JSON line reaches the same stdout — and return the child's exit status.  Under an outer
+    launcher (WORLD_SIZE set) nothing is started.  RE/Scene.h:318-325 is the loop the ranks
+    split."""
+    import subprocess
+    cmd = launcher_command(list(sys.argv[1:] if argv is None else argv), args.gpus, free_port())
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def needs_launcher(args, environ=None) -> bool:
+    env = os.environ if environ is None else environ
+    return args.gpus > 1 and "WORLD_SIZE" not in env
+
+
 def granted_cores() -> int:
     """Cores this process may run on: the affinity mask, capped by OMP_NUM_THREADS when the
     environment sets one (the GPU box grants a 16-core share of a larger machine)."""
@@ -163,7 +195,7 @@ class Runner:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world != args.gpus and self.world > 1:
+        if self.world != args.gpus:
             raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={self.world}")
         torch.cuda.set_device(self.local_rank)
         if self.world > 1:
@@ -377,6 +409,7 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     base = dscene.camera["position"][0].copy()
     static_cams = dscene.cameras([base] * batch)
     nb, nt, nev = [0], [0], [0]
+    last_n = [0, 0]  # frames of the call that last wrote buffer set 0 / 1
 
     # a moving camera's records for the timed frames, formed before the timed region like the
     # static camera's (the camera path is an input of the workload, as the scene is)
@@ -401,6 +434,7 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
             nev[0] += 1
         kw = {"rank_hdr64": local[b & 1].data_ptr()} if hdr == "f64" else \
              {"rank_hdr32": local[b & 1].data_ptr()}
+        last_n[b & 1] = n
         comm.render_gather_batch(dscene, cams_for(f0, n), topts if ev else opts, capi.RT_OUT_LDR,
                                  d_ldr=ldr[b & 1].data_ptr(), **kw)
 
@@ -425,14 +459,20 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
         comm.set_root_weight(1)
     per_frame = [t.render_ms / max(t.frames, 1), t.gather_ms / max(t.frames, 1),
                  t.assemble_ms / max(t.frames, 1), float(rows), float(rays_rank), float(t.frames),
-                 float(nev[0]), t.render_ms]
+                 float(nev[0]), t.render_ms,
+                 # the HIP events on the launch stream around the whole timed region, per frame
+                 # (this rank's render time when no batch carried events of its own)
+                 (region_ms / frames) if region_ms and frames else 0.0]
     ranks = R.gather_rows(per_frame)
     (rays_all,) = R.sum_over_ranks(float(rays_rank))
     dscene.close()
     return {"elapsed": elapsed, "rays": rays_all, "rays_rank": rays_rank, "ranks": ranks,
             "px": W * H, "rows": rows, "frames": frames, "batch": batch,
             "gather_bytes_per_frame": max_rows * W * 3 if split else 0, "root_weight": weight,
-            "region_ms": region_ms, "launches": -(-frames // batch), "bufs": (local, ldr)}
+            "region_ms": region_ms, "launches": -(-frames // batch), "bufs": (local, ldr),
+            "split": split, "V": V, "block": block, "weight": weight,
+            "slots": my_slots if split else [0], "slot_rows": slot_rows, "max_rows": max_rows,
+            "last_n": last_n, "hdr": hdr, "static": camera_step is None}
 
 
 def kernel_ms_per_frame(res, event_every):
@@ -445,14 +485,24 @@ def kernel_ms_per_frame(res, event_every):
 
 def per_rank_summary(res):
     ranks = res["ranks"]
-    render = [r[0] for r in ranks]
-    mean = sum(render) / len(render)
     gb = res.get("gather_bytes_per_frame", 0)
+    def entry(i, r):
+        e = {"rank": i, "rows": int(r[3]), "rays_per_frame": int(r[4])}
+        if int(r[5]) > 0:   # per-batch HIP events (render / gather / assembly)
+            e.update({"render_ms_per_frame": round(r[0], 6),
+                      "gather_ms_per_frame": round(r[1], 6),
+                      "assemble_ms_per_frame": round(r[2], 6), "timed_frames": int(r[5]),
+                      "timing": "HIP events around the event-timed batches"})
+        else:               # no batch carried events: the region's HIP events
+            e.update({"render_ms_per_frame": round(r[8], 6), "timed_frames": res["frames"],
+                      "timing": "HIP events on the launch stream around the whole timed region "
+                                "(render, gather and assembly together, launch gaps included)"})
+        return e
+
+    render = [r[0] if int(r[5]) > 0 else r[8] for r in ranks]
+    mean = sum(render) / len(render)
     out = {
-        "per_rank": [{"rank": i, "rows": int(r[3]), "rays_per_frame": int(r[4]),
-                      "render_ms_per_frame": round(r[0], 6), "gather_ms_per_frame": round(r[1], 6),
-                      "assemble_ms_per_frame": round(r[2], 6), "timed_frames": int(r[5])}
-                     for i, r in enumerate(ranks)],
+        "per_rank": [entry(i, r) for i, r in enumerate(ranks)],
         "render_imbalance": round(max(render) / mean, 4) if mean > 0 else None,
     }
     if gb and len(ranks) > 1:
@@ -463,6 +513,96 @@ def per_rank_summary(res):
         out["gather_GBps_per_rank"] = [round(gb / (r[1] * 1e-3) / 1e9, 2) if r[1] > 0 else None
                                        for r in ranks]
     return out
+
+
+def golden_entry(sc, config: str):
+    """The reference's full-frame record of this config (tests/golden/golden_meta.json, made by
+    the reference compiled in the build container), when the bench's scene is the one it was
+    made from (same scene text, same size); else None."""
+    import hashlib
+    path = os.path.join(HERE, "tests", "golden", "golden_meta.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        info = json.load(fh)["scenes"].get(f"{config}_full")
+    if not info or (info["width"], info["height"]) != (sc.camera.width, sc.camera.height):
+        return None
+    if hashlib.sha256(sc.to_text().encode()).hexdigest() != info["scene_sha256"]:
+        return None
+    return info
+
+
+def block_cyclic_rows(H: int, block: int, V: int, slot: int):
+    """Image rows of row set `slot` of V (blocks of `block` rows, RE/Scene.h:318-325 split by
+    rows), in the order the library packs them."""
+    rows = []
+    for b0 in range(slot * block, H, V * block):
+        rows.extend(range(b0, min(b0 + block, H)))
+    return rows
+
+
+def frame_parity(R: Runner, sc, res, config: str, tonemap: int, tonemap_name: str):
+    """Untimed certification of the timed path's output (after the timed region):
+    * ldr_sha_ok (rank 0): SHA-256 of one assembled frame's tonemapped bytes (frame 0 of the
+      last call into buffer set 0; static camera) == the reference's (golden_meta.json);
+    * ldr_equals_single_gpu (rank 0): the same bytes == a one-launch whole-frame render here;
+    * hdr_rows_ok (every rank, AND over ranks): this rank's rank-local HDR rows of that frame ==
+      the same rows of the whole-frame render on this GPU;
+    * hdr_single_sha_ok (rank 0, f64): that whole-frame render's SHA == the reference's.
+    None = not applicable (no golden for the scene, or a moving camera)."""
+    import hashlib
+    torch, capi = R.torch, R.capi
+    W, H = sc.camera.width, sc.camera.height
+    local, ldr = res["bufs"]
+    info = golden_entry(sc, config)
+    torch.cuda.synchronize()
+    out = {"golden": f"tests/golden/golden_meta.json scenes.{config}_full" if info else None,
+           "frame": "frame 0 of the last call into buffer set 0 (static camera)"}
+    if not res["static"]:
+        return out
+    # the whole frame on this GPU, one launch (rt_render_device), same outputs
+    dscene = R.ctx.scene(sc)
+    hdr_t = torch.float64 if res["hdr"] == "f64" else torch.float32
+    ref_h = torch.empty(H * W * 3, dtype=hdr_t, device="cuda")
+    ref_l = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")
+    with torch.cuda.stream(R.stream):
+        dscene.render_device(ref_h.data_ptr() if res["hdr"] == "f64" else None,
+                             ref_h.data_ptr() if res["hdr"] == "f32" else None,
+                             ref_l.data_ptr(), capi.default_opts(tonemap=tonemap))
+    torch.cuda.synchronize()
+    dscene.close()
+    # this rank's rows, every row set it renders (rank-local outputs: set k at
+    # k * nframes * max_rows * W * 3, nframes = the frames of that call)
+    nf, mr = res["last_n"][0], res["max_rows"]
+    ok = True
+    for k, slot in enumerate(res["slots"]):
+        rows = block_cyclic_rows(H, res["block"], res["V"], slot) if res["split"] else \
+            list(range(H))
+        if not rows:
+            continue
+        off = k * nf * mr * W * 3
+        got = local[0][off:off + len(rows) * W * 3].view(len(rows), W * 3)
+        idx = torch.tensor(rows, dtype=torch.long, device="cuda")
+        want = ref_h.view(H, W * 3).index_select(0, idx)
+        ok = ok and bool(torch.equal(got, want))
+    (worst,) = R.max_over_ranks(0.0 if ok else 1.0)
+    out["hdr_rows_ok"] = worst == 0.0
+    if R.rank == 0:
+        frame = ldr[0][:H * W * 3]
+        out["ldr_equals_single_gpu"] = bool(torch.equal(frame, ref_l))
+        if info:
+            sha = hashlib.sha256(frame.cpu().numpy().tobytes()).hexdigest()
+            want = info["ldr_sha256"].get(tonemap_name)
+            out["ldr_sha_ok"] = (sha == want) if want else None
+            if res["hdr"] == "f64":
+                out["hdr_single_sha_ok"] = hashlib.sha256(
+                    ref_h.cpu().numpy().tobytes()).hexdigest() == info["image_sha256"]
+    return out
+
+
+def parity_failed(p) -> bool:
+    return any(p.get(k) is False for k in ("ldr_sha_ok", "ldr_equals_single_gpu", "hdr_rows_ok",
+                                           "hdr_single_sha_ok"))
 
 
 def single_launch_frames(R: Runner, sc, frames, warmup, tonemap=1):
@@ -525,9 +665,108 @@ def workload_text(sc, world, block, batch, hdr, tonemap_name):
             f"straight into it); {batch} frames per call")
 
 
+def tiled_roofline(t, W, render_ms):
+    """§8(d)'s framebuffer-write roofline of a tiled config's render on rank 0: its rows'
+    bytes per frame (15 B/px = float3 + u8, §8(d); 27 B/px = the f64 Vec3 + u8 written) / its
+    render time per frame (HIP events around every timed batch)."""
+    rows = int(t["ranks"][0][3])
+    if render_ms <= 0:
+        return None
+    out = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "kernel_ms_per_frame": round(render_ms, 6)}
+    for tag, bpp in (("15B", 15), ("27B", 27)):
+        a = rows * W * bpp / (render_ms / 1e3) / 1e9
+        out[f"achieved_{tag}"] = round(a, 2)
+        out[f"frac_{tag}"] = round(a / HBM_PEAK_GBS, 5)
+    return out
+
+
+def _extras(R: Runner, args, sc, line, res, tonemap, batch):
+    """The extra fields of the line (each with its own timing, outside the headline's)."""
+    capi = R.capi
+    from raytracingengine_amd.configs import make_config
+    steps_x = min(args.steps, 96)
+    # one launch per frame: the round-3 headline path
+    v1, ms1, k1 = single_launch_frames(R, sc, steps_x, args.warmup, tonemap)
+    (v1,) = R.sum_over_ranks(v1)
+    line["single_launch"] = {"value": round(v1, 3), "ms_per_frame": round(ms1, 5),
+                             "kernel_ms_per_launch": round(k1, 6),
+                             "note": "every rank its own whole frames, one launch each "
+                                     "(rt_render_device)"}
+    # weak scaling: every rank its own whole frames, batched
+    wk = split_frames(R, sc, steps_x, args.warmup, batch, args.hdr, tonemap, gather=False,
+                      event_every=args.event_every)
+    (rays_w,) = R.sum_over_ranks(float(wk["rays_rank"]))
+    line["weak_frames"] = {
+        "value": round(rays_w * steps_x / wk["elapsed"] / 1e6, 3),
+        "ms_per_step": round(wk["elapsed"] / steps_x * 1e3, 5), "scaling": "weak",
+        "workload": f"{sc.name} whole frames on every rank ({args.hdr} HDR + u8), "
+                    f"{batch} per call"}
+    if R.world == 1:
+        f32 = split_frames(R, sc, steps_x, args.warmup, batch, "f32", tonemap,
+                           event_every=args.event_every)
+        k32 = kernel_ms_per_frame(f32, args.event_every)
+        b32 = res["px"] * 15
+        a32 = b32 / (k32 / 1e3) / 1e9 if k32 > 0 else 0.0
+        line["roofline_f32"] = {
+            "achieved": round(a32, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(a32 / HBM_PEAK_GBS, 5), "alg_bytes_per_frame": b32,
+            "kernel_ms_per_frame": round(k32, 6),
+            "value": round(f32["rays"] * steps_x / f32["elapsed"] / 1e6, 3)}
+        mv = split_frames(R, sc, steps_x, args.warmup, batch, args.hdr, tonemap,
+                          event_every=args.event_every,
+                          camera_step=lambda base, i: base + np.outer(i * 1e-7, (1, 0, 0)))
+        line["moving_camera"] = {
+            "ms_per_step": round(mv["elapsed"] / steps_x * 1e3, 5),
+            "kernel_ms_per_frame": round(kernel_ms_per_frame(mv, args.event_every), 6),
+            "value": round(mv["rays"] * steps_x / mv["elapsed"] / 1e6, 3),
+            "note": "camera x moved by 1e-7 every frame: no frame reuses a cached per-camera "
+                    "packet image (one small launch per batch forms every frame's image "
+                    "before the batch launch, DESIGN §4); rays counted at the first "
+                    "position"}
+        sc1 = make_config("c1", aa=32)
+        v, ms, k = single_launch_frames(R, sc1, 10, 2, capi.TONEMAPS.index("aces"))
+        line["reference_main_c1"] = {
+            "workload": "c1: the reference main() box (5 mirrored axis planes, 2 point "
+                        "lights), 1000x1000, AA=32, f64 Vec3 HDR + fused ACES u8",
+            "ms_per_frame": round(ms, 4), "kernel_ms_per_launch": round(k, 4),
+            "value": round(v, 3), "unit": "Mrays/s"}
+        line["d2h"] = d2h_frames(R, sc, min(args.steps, 20), tonemap)
+    # BASELINE config 3 (SURVEY §8e asks for scaling runs on C2, C3 and C4): the 4K frame,
+    # 128 spheres, 4 point lights, row-tiled through the same path
+    sc3 = make_config("c3", aa=1)
+    n3 = min(args.steps, 32)
+    t3 = split_frames(R, sc3, n3, min(args.warmup, 8), 8, "f64", tonemap, args.row_block,
+                      not args.no_pipeline, 1)
+    line["c3_tiled"] = {
+        "value": round(t3["rays"] * n3 / t3["elapsed"] / 1e6, 3),
+        "ms_per_frame": round(t3["elapsed"] / n3 * 1e3, 5),
+        "frames": n3,
+        "workload": "c3 3840x2160, 128 spheres, 4 planes, 4 point lights, f64 HDR rows on "
+                    "each rank + Reinhard u8 gathered, 8 frames per call",
+        "roofline": tiled_roofline(t3, sc3.camera.width, t3["ranks"][0][0]),
+        **per_rank_summary(t3)}
+    del t3
+    # BASELINE config 4: the 8K frame row-tiled through the same path
+    sc4 = make_config("c4", aa=1)
+    t4 = split_frames(R, sc4, min(args.steps, 16), min(args.warmup, 2), 2, "f64", tonemap,
+                      args.row_block, not args.no_pipeline, 1)
+    line["c4_tiled"] = {
+        "value": round(t4["rays"] * min(args.steps, 16) / t4["elapsed"] / 1e6, 3),
+        "ms_per_frame": round(t4["elapsed"] / min(args.steps, 16) * 1e3, 5),
+        "workload": "c4 7680x4320, 256 spheres, 8 lights, f64 HDR rows on each rank + "
+                    "Reinhard u8 gathered, 2 frames per call",
+        "roofline": tiled_roofline(t4, sc4.camera.width, t4["ranks"][0][0]),
+        **per_rank_summary(t4)}
+
+
 # ------------------------------------------------------------------------------ main
 def main(argv=None):
     args = parse_args(argv)
+    if needs_launcher(args):
+        # --gpus N > 1 without an outer launcher: the N ranks run in ONE child process tree,
+        # started before this process touches the GPU
+        return launch_ranks(args, argv)
     R = Runner(args)
     if args.event_every is None:
         args.event_every = 0 if R.world == 1 else 4
@@ -558,6 +797,9 @@ def main(argv=None):
                        not args.no_pipeline, args.event_every, weight=weight)
     elapsed = res["elapsed"]
     value = res["rays"] * args.steps / elapsed / 1e6
+    # untimed: the timed path's assembled frame and rank-local rows vs the reference's SHA and a
+    # one-launch whole-frame render (every rank takes part)
+    parity = frame_parity(R, sc, res, args.config, tonemap, args.tonemap)
     summ = per_rank_summary(res)
     r0 = res["ranks"][0]
     # the trace kernel: rank 0's render per frame — from HIP events around every
@@ -591,11 +833,21 @@ def main(argv=None):
     traffic_launch = None
     if traffic and R.world == 1:
         traffic_launch = traffic["hbm_bytes_per_launch"] / 32 * frames_per_launch
-    valu, valu_src = load_profile(f"r05_{args.config}_valu.json")
-    if valu is None:
-        valu, valu_src = load_profile(f"r04_{args.config}_valu.json")
-    if valu is None:
-        valu, valu_src = load_profile(f"r03_{args.config}_valu.json")
+    valu, valu_src = None, None
+    for rnd in ("r06", "r05", "r04", "r03"):
+        valu, valu_src = load_profile(f"{rnd}_{args.config}_valu.json")
+        if valu is not None:
+            break
+    # committed counter summaries are from an earlier run: stale when the sources they were
+    # taken from (their recorded rt_build_info digest) are not the ones this run loaded
+    build = {k: v for k, v in capi.build_info().items() if k in
+             ("source_sha256", "matches_tree", "arch", "hipcc")}
+
+    def stale(prof):
+        return prof is None or prof.get("source_sha256") != build.get("source_sha256")
+    if valu is not None:
+        valu = {k: v for k, v in valu.items() if k not in ("counters", "definitions")} | {
+            "definitions": valu.get("definitions"), "stale": stale(valu)}
     line = {
         "metric": "Mrays/sec (primary+shadow) at 1920x1080" if args.config == "c2"
                   else f"Mrays/sec (primary+shadow), config {args.config}",
@@ -619,8 +871,7 @@ def main(argv=None):
         "frames_per_sec": round(args.steps / elapsed, 3),
         # the library this run loaded: the sources it was compiled from (rt_build_info) and
         # whether they are the sources of this tree
-        "build": {k: v for k, v in capi.build_info().items() if k in
-                  ("source_sha256", "matches_tree", "arch", "hipcc")},
+        "build": build,
         "root_weight_probe": probe,
         "clock_warmup_ms": args.clock_warmup_ms,
         "kernel_ms_per_frame": round(render_ms, 6),
@@ -634,6 +885,11 @@ def main(argv=None):
             "alg_bytes_per_launch": round(bytes_per_frame * frames_per_launch),
             "alg_bytes_per_frame": bytes_per_frame,
             "traffic_source": traffic_src if R.world == 1 else None,
+            "traffic_stale": stale(traffic) if traffic_launch else None,
+            # SURVEY §8(d)'s own per-pixel figure: float3 + u8 = 15 B/px (the line's `frac`
+            # counts the bytes this workload writes: the f64 Vec3 framebuffer + u8)
+            "frac_sec8d_15B": round(int(r0[3]) * W * 15 / (render_ms / 1e3) / 1e9 /
+                                    HBM_PEAK_GBS, 5) if render_ms > 0 else None,
             "traffic_note": ("PMC FETCH_SIZE x2 + WRITE_SIZE of a 32-frame launch of this "
                              "config (committed summary), per frame x the frames of the timed "
                              "launch") if traffic_launch else None,
@@ -647,83 +903,18 @@ def main(argv=None):
             "note": "rank 0's batch launch: its rows' framebuffer bytes (HDR + u8) per frame / "
                     f"its render time per frame ({timing_src})",
         },
+        "parity": parity,
         "valu": valu if R.world == 1 else None,
         "valu_source": valu_src if R.world == 1 else None,
         "cpu_baseline": None,
     }
+    if parity_failed(parity):
+        # a wrong frame is not a measurement: print the line (it says which check failed), exit
+        # non-zero, skip the extras
+        extras = False
     if extras:
-        steps_x = min(args.steps, 96)
-        # one launch per frame: the round-3 headline path
-        v1, ms1, k1 = single_launch_frames(R, sc, steps_x, args.warmup, tonemap)
-        (v1,) = R.sum_over_ranks(v1)
-        line["single_launch"] = {"value": round(v1, 3), "ms_per_frame": round(ms1, 5),
-                                 "kernel_ms_per_launch": round(k1, 6),
-                                 "note": "every rank its own whole frames, one launch each "
-                                         "(rt_render_device)"}
-        # weak scaling: every rank its own whole frames, batched
-        wk = split_frames(R, sc, steps_x, args.warmup, batch, args.hdr, tonemap, gather=False,
-                          event_every=args.event_every)
-        (rays_w,) = R.sum_over_ranks(float(wk["rays_rank"]))
-        line["weak_frames"] = {
-            "value": round(rays_w * steps_x / wk["elapsed"] / 1e6, 3),
-            "ms_per_step": round(wk["elapsed"] / steps_x * 1e3, 5), "scaling": "weak",
-            "workload": f"{sc.name} whole frames on every rank ({args.hdr} HDR + u8), "
-                        f"{batch} per call"}
-        if R.world == 1:
-            f32 = split_frames(R, sc, steps_x, args.warmup, batch, "f32", tonemap,
-                               event_every=args.event_every)
-            k32 = kernel_ms_per_frame(f32, args.event_every)
-            b32 = res["px"] * 15
-            a32 = b32 / (k32 / 1e3) / 1e9 if k32 > 0 else 0.0
-            line["roofline_f32"] = {
-                "achieved": round(a32, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(a32 / HBM_PEAK_GBS, 5), "alg_bytes_per_frame": b32,
-                "kernel_ms_per_frame": round(k32, 6),
-                "value": round(f32["rays"] * steps_x / f32["elapsed"] / 1e6, 3)}
-            mv = split_frames(R, sc, steps_x, args.warmup, batch, args.hdr, tonemap,
-                              event_every=args.event_every,
-                              camera_step=lambda base, i: base + np.outer(i * 1e-7, (1, 0, 0)))
-            line["moving_camera"] = {
-                "ms_per_step": round(mv["elapsed"] / steps_x * 1e3, 5),
-                "kernel_ms_per_frame": round(kernel_ms_per_frame(mv, args.event_every), 6),
-                "value": round(mv["rays"] * steps_x / mv["elapsed"] / 1e6, 3),
-                "note": "camera x moved by 1e-7 every frame: no frame reuses a cached per-camera "
-                        "packet image (one small launch per batch forms every frame's image "
-                        "before the batch launch, DESIGN §4); rays counted at the first "
-                        "position"}
-            sc1 = make_config("c1", aa=32)
-            v, ms, k = single_launch_frames(R, sc1, 10, 2, capi.TONEMAPS.index("aces"))
-            line["reference_main_c1"] = {
-                "workload": "c1: the reference main() box (5 mirrored axis planes, 2 point "
-                            "lights), 1000x1000, AA=32, f64 Vec3 HDR + fused ACES u8",
-                "ms_per_frame": round(ms, 4), "kernel_ms_per_launch": round(k, 4),
-                "value": round(v, 3), "unit": "Mrays/s"}
-            line["d2h"] = d2h_frames(R, sc, min(args.steps, 20), tonemap)
-        # BASELINE config 3 (SURVEY §8e asks for scaling runs on C2, C3 and C4): the 4K frame,
-        # 128 spheres, 4 point lights, row-tiled through the same path
-        sc3 = make_config("c3", aa=1)
-        n3 = min(args.steps, 32)
-        t3 = split_frames(R, sc3, n3, min(args.warmup, 8), 8, "f64", tonemap, args.row_block,
-                          not args.no_pipeline, 1)
-        line["c3_tiled"] = {
-            "value": round(t3["rays"] * n3 / t3["elapsed"] / 1e6, 3),
-            "ms_per_frame": round(t3["elapsed"] / n3 * 1e3, 5),
-            "frames": n3,
-            "workload": "c3 3840x2160, 128 spheres, 4 planes, 4 point lights, f64 HDR rows on "
-                        "each rank + Reinhard u8 gathered, 8 frames per call",
-            **per_rank_summary(t3)}
-        del t3
-        # BASELINE config 4: the 8K frame row-tiled through the same path
-        sc4 = make_config("c4", aa=1)
-        t4 = split_frames(R, sc4, min(args.steps, 16), min(args.warmup, 2), 2, "f64", tonemap,
-                          args.row_block, not args.no_pipeline, 1)
-        line["c4_tiled"] = {
-            "value": round(t4["rays"] * min(args.steps, 16) / t4["elapsed"] / 1e6, 3),
-            "ms_per_frame": round(t4["elapsed"] / min(args.steps, 16) * 1e3, 5),
-            "workload": "c4 7680x4320, 256 spheres, 8 lights, f64 HDR rows on each rank + "
-                        "Reinhard u8 gathered, 2 frames per call",
-            **per_rank_summary(t4)}
-    if R.world == 1 and not args.no_cpu_baseline:
+        _extras(R, args, sc, line, res, tonemap, batch)
+    if R.world == 1 and not args.no_cpu_baseline and not parity_failed(parity):
         try:
             line["cpu_baseline"] = cpu_baseline(sc, res["rays_rank"], args.cpu_frames)
         except Exception as e:  # a reported baseline, never the product path
@@ -731,7 +922,8 @@ def main(argv=None):
     if R.rank == 0:
         print(json.dumps(line), flush=True)
     R.close()
+    return 3 if parity_failed(parity) else 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

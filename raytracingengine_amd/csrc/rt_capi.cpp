@@ -442,6 +442,23 @@ rt_status packet_batch_images(rt_context* ctx, const rt_scene* sc, const rt_came
     bool same_cam = true;
     bool any_ring = false;
     const size_t cache_before = sc->pk_images.size();
+    // Every error exit after the first promotion drops the entries this call created (newest
+    // last): an entry that never received its image, with a `ready` event never recorded, would
+    // be taken as a formed image by every later render from that camera position.
+    struct Rollback {
+        const rt_scene* sc;
+        size_t keep;
+        bool armed = true;
+        ~Rollback() {
+            if (!armed) return;
+            while (sc->pk_images.size() > keep) {
+                auto& im = sc->pk_images.back();
+                im.buf.release();
+                if (im.ready) (void)hipEventDestroy(im.ready);
+                sc->pk_images.pop_back();
+            }
+        }
+    } rollback{sc, cache_before};
     for (int f = 0; f < nframes; ++f) {
         PkFrame& F = p.fr[f];
         for (int i = 0; i < 3; ++i) F.cam[i] = cams[f].position[i];
@@ -505,16 +522,8 @@ rt_status packet_batch_images(rt_context* ctx, const rt_scene* sc, const rt_came
     hipError_t e = launch_packet_image_batch(p, jobs, ctx->stream);
     for (int f = 0; f < nframes && e == hipSuccess; ++f)
         if (kind[f] == kPromote) e = hipEventRecord(ent[f]->ready, ctx->stream);
-    if (e != hipSuccess) {
-        // the entries this call created never received their image: drop them (newest last)
-        while (sc->pk_images.size() > cache_before) {
-            auto& im = sc->pk_images.back();
-            im.buf.release();
-            if (im.ready) (void)hipEventDestroy(im.ready);
-            sc->pk_images.pop_back();
-        }
-        return hip_fail(e, "packet batch images");
-    }
+    if (e != hipSuccess) return hip_fail(e, "packet batch images");  // the rollback drops them
+    rollback.armed = false;  // every promoted entry now has its image and its recorded event
     if (kind[0] == kCached) return tile_order(ctx, *ent[0], p, flags, rec, !same_cam);
     return scene_tile_order(ctx, sc, p, flags, rec);
 }
@@ -552,8 +561,11 @@ rt_status fixup_buffers(rt_context* ctx, size_t px, TraceParams& p) {
         RT_HIP(hipMemsetAsync(ctx->fix_ctl.ptr, 0, 2 * sizeof(uint32_t), ctx->stream));
     }
     if (ctx->fix_list.bytes < px * sizeof(uint32_t)) {
-        // the list may still be read by a fix-up launch on any stream the context used
-        RT_HIP(hipDeviceSynchronize());
+        // the list may still be read by a fix-up launch on any stream the context used; every
+        // user of the list is a scratch user, so the context's last scratch event covers them
+        // all (not hipDeviceSynchronize: it would also wait on an RCCL gather of a dead peer
+        // and on other contexts' work)
+        if (ctx->scratch_used) RT_HIP(hipEventSynchronize(ctx->scratch_event));
         RT_HIP(ctx->fix_list.ensure(px * sizeof(uint32_t)));
     }
     p.fix_list = static_cast<uint32_t*>(ctx->fix_list.ptr);
@@ -692,23 +704,34 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
         const char* env = std::getenv("RTAMD_WF_MB");
         const size_t budget = (env && std::atoll(env) > 0 ? static_cast<size_t>(std::atoll(env))
                                                           : size_t(4096)) << 20;
-        const size_t root_bytes = wf_arena_bytes(n0, n0);
+        // the deferred-direct queue is laid out only when that pass runs (refraction trees)
+        const bool defer = path == kPathTree && wf_defer_selected();
+        const size_t root_bytes = wf_arena_bytes(n0, n0, defer);
         if (n0 < (size_t(1) << 30) && root_bytes <= budget) {
-            size_t extra = (budget - root_bytes) / 100;  // ~100 B per non-root node
+            // ~100 B per non-root node (+16 B of queue when deferred)
+            size_t extra = (budget - root_bytes) / (defer ? 116 : 100);
             extra = std::min(extra, std::max<size_t>(n0, 1) * 64);
             extra = std::min(extra, (size_t(1) << 31) - 1 - n0);
             const size_t cap = n0 + extra;
-            RT_HIP(ctx->wf.ensure(wf_arena_bytes(n0, cap)));
+            RT_HIP(ctx->wf.ensure(wf_arena_bytes(n0, cap, defer)));
             RT_HIP(ctx->wf_ctl.ensure(sizeof(WfCtl)));
             const WfArena A = wf_arena_layout(ctx->wf.ptr, n0, cap,
-                                              static_cast<WfCtl*>(ctx->wf_ctl.ptr));
+                                              static_cast<WfCtl*>(ctx->wf_ctl.ptr), defer);
             RT_HIP(lean_generic ? lean::launch_wavefront(p, path, A, lds, lds_bytes, ctx->stream)
                                 : launch_wavefront(p, path, A, lds, lds_bytes, ctx->stream));
             wavefront = true;
         }
     }
     if (!wavefront) RT_HIP(launch(p, false));
-    if (fixup) RT_HIP(launch_packet_fixup(p, ctx->stream));
+    if (fixup) {
+        const hipError_t fe = launch_packet_fixup(p, ctx->stream);
+        if (fe != hipSuccess) {
+            // the packet launch appended to the list and nothing will zero its count: reset it,
+            // or the next fix-variant launch would append at a stale base past its list
+            (void)hipMemsetAsync(ctx->fix_ctl.ptr, 0, 2 * sizeof(uint32_t), ctx->stream);
+            return hip_fail(fe, "launch_packet_fixup");
+        }
+    }
     if (rec) RT_HIP(hipEventRecord(rec->recorded, ctx->stream));
     if (flags & RT_FLAG_TIME_KERNEL) {
         RT_HIP(hipEventRecord(ev.second, ctx->stream));

@@ -1121,7 +1121,11 @@ rt_status rt_comm_set_root_weight(rt_comm* c, int weight) {
         st = rt_comm_synchronize(c);
         if (st != RT_OK) return st;
     }
-    if (c->nccl && c->nranks > 1) {
+    if (c->nccl && c->nonblocking && c->nranks > 1) {
+        // Only rt_comm_create communicators (one process per GPU, non-blocking init) agree here:
+        // rt_comm_create_all / create_local ranks are driven serially from one thread, so an
+        // all-reduce enqueued on one of them alone would never complete; their weights are
+        // checked on the host by rt_render_gather_all_batch instead.
         // Collective on a communicator of one process per GPU: every rank must plan the same
         // split (a peer sizing its send from another weight than rank 0's receive would read
         // past buffers or pair ncclSend with ncclGather and hang), so the ranks agree on it

@@ -520,17 +520,24 @@ hipError_t launch_levels(const TraceParams& p, const WfArena& A, size_t lds_byte
 }  // namespace
 
 #ifndef RT_LEAN_GENERIC
-size_t wf_arena_bytes(size_t n0, size_t cap) {
-    const size_t cap_r = cap - n0;
-    return sizeof(double) * (6 * cap + 6 * cap_r) + sizeof(int32_t) * 4 * cap +
-           sizeof(uint32_t) * cap_r + n0 + 64;
+bool wf_defer_selected() {
+    const char* defer_env = std::getenv("RTAMD_WF_DEFER");
+    return defer_env && std::atoi(defer_env) == 1;
 }
 
-WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl) {
+size_t wf_arena_bytes(size_t n0, size_t cap, bool defer) {
+    const size_t cap_r = cap - n0;
+    return sizeof(double) * (5 * cap + 6 * cap_r) + sizeof(int32_t) * 2 * cap +
+           sizeof(uint32_t) * cap_r + (defer ? (sizeof(double) + 2 * sizeof(uint32_t)) * cap : 0) +
+           n0 + 64;
+}
+
+WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl, bool defer) {
     WfArena A;
     A.n0 = static_cast<uint32_t>(n0);
     A.cap = static_cast<uint32_t>(cap);
     A.cap_r = static_cast<uint32_t>(cap - n0);
+    A.defer = defer;
     char* q = static_cast<char*>(mem);
     A.val = reinterpret_cast<double*>(q);
     q += sizeof(double) * 3 * cap;
@@ -540,16 +547,22 @@ WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl) {
     q += sizeof(double) * cap;
     A.ray = reinterpret_cast<double*>(q);
     q += sizeof(double) * 6 * A.cap_r;
-    A.dq_t = reinterpret_cast<double*>(q);
-    q += sizeof(double) * cap;
+    A.dq_t = nullptr;
+    if (defer) {
+        A.dq_t = reinterpret_cast<double*>(q);
+        q += sizeof(double) * cap;
+    }
     A.child = reinterpret_cast<int32_t*>(q);
     q += sizeof(int32_t) * 2 * cap;
     A.root = reinterpret_cast<uint32_t*>(q);
     q += sizeof(uint32_t) * A.cap_r;
-    A.dq_id = reinterpret_cast<uint32_t*>(q);
-    q += sizeof(uint32_t) * cap;
-    A.dq_code = reinterpret_cast<uint32_t*>(q);
-    q += sizeof(uint32_t) * cap;
+    A.dq_id = A.dq_code = nullptr;
+    if (defer) {
+        A.dq_id = reinterpret_cast<uint32_t*>(q);
+        q += sizeof(uint32_t) * cap;
+        A.dq_code = reinterpret_cast<uint32_t*>(q);
+        q += sizeof(uint32_t) * cap;
+    }
     A.redo = reinterpret_cast<uint8_t*>(q);
     A.ctl = ctl;
     return A;
@@ -564,8 +577,7 @@ hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bo
     // deferred direct lighting for refraction trees (RTAMD_WF_DEFER=1; off by default: measured
     // on glass 994 vs 971 us per frame, the level kernels 848 -> 480 us but the direct pass 390 us,
     // profiles/r05_glass_defer.txt)
-    const char* defer_env = std::getenv("RTAMD_WF_DEFER");  // read per frame (tests switch it)
-    const bool defer = defer_env && std::atoi(defer_env) == 1;
+    const bool defer = A.defer;  // wf_defer_selected() when the arena was laid out
     // (the queue's hit code holds a primitive index below 2^26 and a level below 16)
     static_assert(kMaxDepth <= 16, "dq_code level bits");
     const bool fits = p.ns < (1 << 26) && p.np < (1 << 26) && p.nt < (1 << 26);

@@ -32,15 +32,19 @@ struct WfArena {
     // < 1, appended by the level kernels — node id, hit code (primitive index | kind << 26 |
     // level << 28), hit distance — and shaded by wf_direct_kernel after the last level; the
     // last shading level's records fill the queue from the back
-    uint32_t* dq_id;    // cap
-    uint32_t* dq_code;  // cap
-    double* dq_t;       // cap
+    uint32_t* dq_id;    // cap (null unless `defer`)
+    uint32_t* dq_code;  // cap (null unless `defer`)
+    double* dq_t;       // cap (null unless `defer`)
     WfCtl* ctl;
     uint32_t n0, cap, cap_r;
+    bool defer;         // the arena holds the deferred-direct queue (wf_defer_selected())
 };
 
-size_t wf_arena_bytes(size_t n0, size_t cap);
-WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl);
+// Whether refraction trees take the deferred direct-lighting pass (RTAMD_WF_DEFER=1; read per
+// frame, tests switch it).  The arena is sized and laid out for the queue only then.
+bool wf_defer_selected();
+size_t wf_arena_bytes(size_t n0, size_t cap, bool defer);
+WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl, bool defer);
 hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bool lds,
                             size_t lds_bytes, hipStream_t stream);
 namespace lean {  // rt_wavefront_lean.hip: scenes without triangles / area light

@@ -541,3 +541,57 @@ def test_fixup_variant_vs_oracle_on_undecided_shadows(ctx, oracle, monkeypatch):
     for f in range(n):
         assert np.array_equal(got64[f], ref), f
         assert np.array_equal(got8[f], ref8), f
+
+
+@pytest.mark.parametrize("pipeline", [True, False])
+def test_c4_own_shape_8_local_ranks_is_the_reference(ctx, golden, pipeline):
+    """BASELINE config 4 in its own shape: 7680x4320, 256 spheres, 8 point lights, split over 8
+    ranks in block-cyclic 16-row blocks (the 256-thread 16x16-px workgroup variant of the packet
+    kernel), through 8 local communicators on this one GPU (rt_comm_create_local: the gather as
+    device copies, the same plan, padded send rows and assembly launch as the RCCL path).  Three
+    calls of 2 static-camera frames — first sighting (publish slots), cache-creating and cached
+    camera — and every assembled frame's HDR and Reinhard bytes have the reference's SHA-256
+    (RE/Scene.h:311-328; golden_meta.json c4_full)."""
+    info = golden["meta"]["scenes"]["c4_full"]
+    n, nf, block = 8, 2, 16
+    ctxs = [capi.Context(0) for _ in range(n)]
+    try:
+        comms = capi.Comm.create_local(ctxs)
+        sc = make_config("c4")
+        W, H = sc.camera.width, sc.camera.height
+        assert (W, H) == (info["width"], info["height"])
+        scenes = [c.scene(sc) for c in ctxs]
+        cams = scenes[0].cameras(np.repeat(scenes[0].camera["position"], nf, axis=0))
+        opts = capi.default_opts(tonemap=1, row_block=block,
+                                 flags=capi.RT_FLAG_PIPELINE if pipeline else 0)
+        H64 = torch.empty(nf * H * W * 3, dtype=torch.float64, device="cuda")
+        L8 = torch.empty(nf * H * W * 3, dtype=torch.uint8, device="cuda")
+        first = None
+        for rnd in range(3):
+            H64.fill_(-1.0)
+            L8.zero_()
+            torch.cuda.synchronize()
+            capi.render_gather_all_batch(comms, scenes, cams, opts,
+                                         capi.RT_OUT_LDR | capi.RT_OUT_HDR64,
+                                         d_hdr64=H64.data_ptr(), d_ldr=L8.data_ptr())
+            for c in comms:
+                c.synchronize()
+            torch.cuda.synchronize()
+            h = H64.view(nf, -1)
+            l8 = L8.view(nf, -1)
+            if first is None:
+                # the SHA of the first frame on the host, every other frame equal to it on the GPU
+                assert _sha(h[0].cpu().numpy()) == info["image_sha256"]
+                assert _sha(l8[0].cpu().numpy()) == info["ldr_sha256"]["reinhard_simple"]
+                first = (h[0].clone(), l8[0].clone())
+            for f in range(nf):
+                assert torch.equal(h[f], first[0]), (rnd, f)
+                assert torch.equal(l8[f], first[1]), (rnd, f)
+        del H64, L8, first
+        for s in scenes:
+            s.close()
+        for c in comms:
+            c.close()
+    finally:
+        for c in ctxs:
+            c.close()

@@ -390,3 +390,42 @@ def test_comm_with_deadline_renders_and_synchronizes(ctx):
         assert e.value.status == capi.RT_ERR_INVALID_ARG
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("weight", [1, 2])
+def test_create_all_set_root_weight_then_weighted_gather(ctx, weight):
+    """rt_comm_set_root_weight on every communicator of an rt_comm_create_all group (blocking
+    ncclCommInitAll ranks driven serially from one thread) must not enqueue the agreement
+    all-reduce — only rt_comm_create ranks (one process per GPU) agree through RCCL; this group's
+    weights are checked on the host by rt_render_gather_all_batch.  Then a weighted batch over
+    the group equals the single-GPU frames.  Every device of the box (one on the test box: the
+    call path; all of them on a multi-GPU node: the weighted P2P split over RCCL)."""
+    ndev = torch.cuda.device_count()
+    ctxs = [capi.Context(d) for d in range(ndev)]
+    try:
+        comms = capi.Comm.create_all(ctxs)
+        for c in comms:
+            c.set_root_weight(weight)   # returns at once (no collective to hang on)
+        sc = make_config("c2", 480, 270)
+        W, H, nf = 480, 270, 3
+        scenes = [c.scene(sc) for c in ctxs]
+        ref = scenes[0].render(hdr64=True, tonemap=1)
+        cams = scenes[0].cameras(np.repeat(scenes[0].camera["position"], nf, axis=0))
+        with torch.cuda.device(0):
+            L8 = torch.zeros(nf * H * W * 3, dtype=torch.uint8, device="cuda:0")
+            H64 = torch.zeros(nf * H * W * 3, dtype=torch.float64, device="cuda:0")
+        capi.render_gather_all_batch(comms, scenes, cams, capi.default_opts(tonemap=1, row_block=16),
+                                     capi.RT_OUT_LDR | capi.RT_OUT_HDR64,
+                                     d_hdr64=H64.data_ptr(), d_ldr=L8.data_ptr())
+        for c in comms:
+            c.synchronize()
+        for f in range(nf):
+            assert np.array_equal(H64.view(nf, -1)[f].cpu().numpy(), ref["hdr64"].reshape(-1)), f
+            assert np.array_equal(L8.view(nf, -1)[f].cpu().numpy(), ref["ldr"].reshape(-1)), f
+        for s in scenes:
+            s.close()
+        for c in comms:
+            c.close()
+    finally:
+        for c in ctxs:
+            c.close()

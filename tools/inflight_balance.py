@@ -113,6 +113,8 @@ for name in CONFIGS:
         ds.render_device(bufs[0][0].data_ptr(), None, bufs[0][1].data_ptr(), full_o)
     BUSY, FULL_O = bufs[0], full_o
     cyc = 64  # whole frames (~3 ms of C2) ahead of every measured run
+    # batches whose two buffer sets fit 16 GiB (C4: up to 8 frames per launch)
+    batches = [G for G in BATCHES if 2 * G * W * H * 27 <= 16 << 30] or [1]
     full = {}
     for S in STREAMS:
         warm(ds, full_o, bufs, 30)
@@ -133,7 +135,7 @@ for name in CONFIGS:
         out["ranks_ms"][S] = [round(t, 5) for t in ts]
         out["host_us"][S] = round(sum(hs) / n, 2)
         out.setdefault("max_rank_over_full_div_n", {})[S] = round(max(ts) / (full[1][0] / n), 3)
-    for G in BATCHES:
+    for G in batches:
         bbufs = [(torch.empty(G * W * H * 3, dtype=torch.float64, device="cuda"),
                   torch.empty(G * W * H * 3, dtype=torch.uint8, device="cuda")) for _ in range(2)]
         warm(ds, full_o, bufs, 30)
@@ -151,8 +153,8 @@ for name in CONFIGS:
         out.setdefault("batch_max_rank_over_full_div_n", {})[G] = round(max(ts) / (full[1][0] / n), 3)
         del bbufs
     # the weighted split (rt_comm_set_root_weight): rank 0 renders w of the w + n − 1 row sets
-    # (one batch launch per set), every other rank one — measured per frame at 32-frame batches
-    G = 32
+    # (one batch launch per set), every other rank one — measured per frame at the largest batch
+    G = batches[-1]
     bbufs = [(torch.empty(G * W * H * 3, dtype=torch.float64, device="cuda"),
               torch.empty(G * W * H * 3, dtype=torch.uint8, device="cuda")) for _ in range(2)]
     Tb = out["batch_full_frame_ms"][G]

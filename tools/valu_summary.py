@@ -18,8 +18,13 @@ FP64_PEAK_TFLOPS = 78.6  # 1024 SIMDs x 16 lanes x 2 flops x 2.4 GHz (FMA); FP32
 def main():
     summ, sub, dur_ns, out = sys.argv[1], sys.argv[2], float(sys.argv[3]), sys.argv[4]
     d = json.load(open(summ))
-    (name, c), = [(k, v) for k, v in d.items() if sub in k]
+    (name, c), = [(k, v) for k, v in d.items() if sub in k and not k.startswith("_")]
     cap = SIMDS * dur_ns * 1e-9 * CLOCK
+    # the clock the chip ran at during the passes: GRBM_GUI_ACTIVE (GPU-busy cycles, summed
+    # over the 8 XCDs) / 8 / duration; the SIMD capacity at that clock is what the issue
+    # cycles are measured against
+    clk = c["GRBM_GUI_ACTIVE"] / 8 / (dur_ns * 1e-9) if c.get("GRBM_GUI_ACTIVE") else CLOCK
+    cap_clk = SIMDS * dur_ns * 1e-9 * clk
     f64 = c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_FMA_F64"]
     trans = c["SQ_INSTS_VALU_TRANS_F64"]
     other = c["SQ_INSTS_VALU"] - f64 - trans
@@ -32,20 +37,29 @@ def main():
         "valu_per_wave": round(c["SQ_INSTS_VALU"] / waves, 1),
         "salu_per_wave": round(c["SQ_INSTS_SALU"] / waves, 1),
         "fp64_share_of_valu": round((f64 + trans) / c["SQ_INSTS_VALU"], 4),
-        "valu_busy_frac": round(4 * c["SQ_ACTIVE_INST_VALU"] / cap, 4),
-        "valu_issue_frac": round(issue / cap, 4),
+        "clock_ghz_measured": round(clk / 1e9, 4),
+        "valu_issue_frac": round(issue / cap_clk, 4),
+        "valu_issue_frac_at_2p4ghz": round(issue / cap, 4),
+        "active_inst_valu_ratio": round(4 * c["SQ_ACTIVE_INST_VALU"] / cap_clk, 4),
         "fp64_counted_tflops": round(flops / (dur_ns * 1e-9) / 1e12, 3),
         "fp64_counted_frac": round(flops / (dur_ns * 1e-9) / 1e12 / FP64_PEAK_TFLOPS, 4),
         "definitions": {
-            "valu_busy_frac": "4 x SQ_ACTIVE_INST_VALU (quad-cycles) / (1024 SIMDs x duration x "
-                              "2.4 GHz): share of SIMD cycles executing a VALU instruction",
-            "valu_issue_frac": "(4 x FP64 add/mul/fma + 16 x FP64 transcendental + 2 x other "
-                               "VALU wave-instructions) / the same capacity: the issue-rate "
-                               "roofline of the kernel's instruction mix",
+            "valu_issue_frac": "issue cycles (4 x FP64 add/mul/fma + 16 x FP64 transcendental + "
+                               "2 x other VALU wave-instructions, the per-class costs measured "
+                               "by tools/micro) / SIMD cycles (1024 SIMDs x duration x the "
+                               "measured clock, clock_ghz_measured = GRBM_GUI_ACTIVE / 8 / "
+                               "duration): the share of SIMD cycles the kernel's VALU "
+                               "instructions occupy, a fraction <= 1",
+            "valu_issue_frac_at_2p4ghz": "the same issue cycles against the 2.4 GHz peak clock",
+            "active_inst_valu_ratio": "4 x SQ_ACTIVE_INST_VALU / the measured-clock SIMD cycles: "
+                                      "NOT a busy fraction (the counter is not SIMD-busy cycles; "
+                                      "it exceeds 1 on saturated kernels), kept for comparison "
+                                      "with earlier rounds' valu_busy_frac",
             "fp64_counted_tflops": "64 flops per FP64 add/mul and 128 per FMA wave-instruction "
                                    "(all lanes counted) / duration, against 78.6 TF",
         },
         "counters": c,
+        "source_sha256": d.get("_build", {}).get("source_sha256"),
     }
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k not in ("counters", "definitions")}))
