@@ -595,3 +595,44 @@ def test_c4_own_shape_8_local_ranks_is_the_reference(ctx, golden, pipeline):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize("fix", ["1", "0"])
+def test_zero_step_shadow_origins_vs_oracle(ctx, oracle, monkeypatch, fix):
+    """Shadow origins lying exactly on a plane: in C2 the ~1 600 floor hits of row 780, where the
+    floor meets the back wall (z = 15), start their shadow ray on the back wall, whose t = ±0 is
+    the march's first closest hit (Scene.h:51-55: origin += direction·bias, traveled = bias) —
+    every undecided lane of a C2 frame is one of them (the packet classifier leaves them to the
+    exact march, or in the fix-up variant to packet_fixup_kernel).  With C2's own light and two
+    lights placed just above two such pixels — one closer than 2·bias (traveled = bias >=
+    maxDist ends the march: clear) and one a little farther — the rows around the corner equal
+    the C oracle bit for bit, through the fix-up variant (a batch) and the marching variant."""
+    monkeypatch.setenv("RTAMD_PK_FIX", fix)
+    sc = make_config("c2")
+    # floor / back-wall corner pixels of row 780 (P = (x − 960)/24, −10, 15) for x = 874, 1614
+    sc.add_light((-3.5833333333333335, -10.0 + 1.5e-3, 15.0 - 2e-4), (1.0, 1.0, 1.0), 0.5)
+    sc.add_light((27.25, -10.0 + 3e-3, 15.0 - 1e-3), (1.0, 0.5, 0.25), 0.5)
+    W, r0, r1 = sc.camera.width, 776, 784
+    rows = r1 - r0
+    ds = ctx.scene(sc)
+    n = 2 if fix == "1" else 1
+    try:
+        opts = capi.default_opts(tonemap=1, row_begin=r0, row_end=r1)
+        H64 = torch.full((n * rows * W * 3,), -1.0, dtype=torch.float64, device="cuda")
+        L8 = torch.zeros(n * rows * W * 3, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        if n > 1:
+            ds.render_batch(ds.cameras(np.repeat(ds.camera["position"], n, axis=0)),
+                            H64.data_ptr(), None, L8.data_ptr(), opts)
+        else:
+            ds.render_device(H64.data_ptr(), None, L8.data_ptr(), opts)
+        ctx.synchronize()
+        got64 = H64.cpu().numpy().reshape(n, rows, W, 3)
+        got8 = L8.cpu().numpy().reshape(n, -1)
+    finally:
+        ds.close()
+    ref, _, _ = oracle.render(sc, rows=(r0, r1))
+    ref8 = oracle.tonemap(ref, 1).reshape(-1)
+    for f in range(n):
+        assert np.array_equal(got64[f], ref), f
+        assert np.array_equal(got8[f], ref8), f
