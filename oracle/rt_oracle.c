@@ -71,10 +71,22 @@ static inline uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+/* Per pixel a 64-bit splitmix64 finalizer folded to a 32-bit key, per (key, stream) and per draw
+ * a 32-bit lowbias32 finalizer (the device's u01, rt_device.hpp).  h * 2^-32 in [0, 1). */
+static inline uint32_t hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
 double oracle_u01(uint64_t seed, uint64_t pixel, uint32_t stream, uint32_t index) {
-    uint64_t h = mix64(seed ^ (0x9E3779B97F4A7C15ULL * (pixel + 1ULL)));
-    h = mix64(h ^ (((uint64_t)stream << 32) | (uint64_t)index));
-    return (double)(h >> 11) * 0x1.0p-53;
+    const uint64_t k = mix64(seed ^ (0x9E3779B97F4A7C15ULL * (pixel + 1ULL)));
+    const uint32_t key = (uint32_t)(k ^ (k >> 32));
+    const uint32_t skey = hash32(key ^ (stream * 0x9E3779B9U));
+    return (double)hash32(skey + index * 0x85EBCA6BU) * 0x1.0p-32;
 }
 
 /* ---------------------------------------------------------------- intersections */

@@ -110,9 +110,18 @@ inline double jitter_u01(uint64_t seed, uint64_t pixel, uint32_t stream, uint32_
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
         return z ^ (z >> 31);
     };
-    uint64_t h = mix(seed ^ (0x9E3779B97F4A7C15ULL * (pixel + 1ULL)));
-    h = mix(h ^ ((static_cast<uint64_t>(stream) << 32) | index));
-    return static_cast<double>(h >> 11) * 0x1.0p-53;
+    auto hash32 = [](uint32_t x) {
+        x ^= x >> 16;
+        x *= 0x7feb352dU;
+        x ^= x >> 15;
+        x *= 0x846ca68bU;
+        x ^= x >> 16;
+        return x;
+    };
+    const uint64_t k = mix(seed ^ (0x9E3779B97F4A7C15ULL * (pixel + 1ULL)));
+    const uint32_t key = static_cast<uint32_t>(k ^ (k >> 32));
+    const uint32_t skey = hash32(key ^ (stream * 0x9E3779B9U));
+    return static_cast<double>(hash32(skey + index * 0x85EBCA6BU)) * 0x1.0p-32;
 }
 }  // namespace rtamd
 

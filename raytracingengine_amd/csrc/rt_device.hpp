@@ -233,22 +233,40 @@ __device__ __forceinline__ d3 refract(d3 v, d3 n, double eta) {
 }
 
 // Build-defined counter RNG (the reference's jitter is an unseeded mt19937, Math.h:109-112).
-// Identical integer arithmetic to oracle_u01 so AA>1 and area-light renders are reproducible.
+// Identical integer arithmetic to oracle_u01 (oracle/rt_oracle.c) and rtamd::jitter_u01
+// (api/rtamd/math.hpp), so AA>1 and area-light renders are reproducible.  Per pixel one 64-bit
+// splitmix64 finalizer of (seed, pixel) folded to a 32-bit key; per (key, stream) and per draw
+// one 32-bit finalizer each (lowbias32: x ^= x >> 16, ×0x7feb352d, x ^= x >> 15, ×0x846ca68b,
+// x ^= x >> 16 — a bijection of 2^32 with full avalanche).  A draw is h·2^-32 ∈ [0, 1) (32-bit
+// resolution).  Round 6: this replaced two 64-bit finalizers per draw (eight 64-bit multiplies,
+// 32 quarter-rate 32-bit multiplies on the VALU): the key and the stream's key are loop
+// invariants of a pixel's sample loops, so a draw costs two 32-bit multiplies.
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ uint64_t pixel_key(uint64_t seed, uint64_t pixel) {
-    return mix64(seed ^ (0x9E3779B97F4A7C15ULL * (pixel + 1ULL)));
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
 }
-__device__ __forceinline__ double u01_key(uint64_t key, uint32_t stream, uint32_t index) {
-    const uint64_t h = mix64(key ^ ((static_cast<uint64_t>(stream) << 32) | index));
-    return static_cast<double>(h >> 11) * 0x1.0p-53;
+__device__ __forceinline__ uint32_t pixel_key(uint64_t seed, uint64_t pixel) {
+    const uint64_t k = mix64(seed ^ (0x9E3779B97F4A7C15ULL * (pixel + 1ULL)));
+    return static_cast<uint32_t>(k ^ (k >> 32));
+}
+__device__ __forceinline__ uint32_t stream_key(uint32_t key, uint32_t stream) {
+    return hash32(key ^ (stream * 0x9E3779B9U));
+}
+__device__ __forceinline__ double u01_skey(uint32_t skey, uint32_t index) {
+    return static_cast<double>(hash32(skey + index * 0x85EBCA6BU)) * 0x1.0p-32;
 }
 __device__ __forceinline__ double u01(uint64_t seed, uint64_t pixel, uint32_t stream,
                                       uint32_t index) {
-    return u01_key(pixel_key(seed, pixel), stream, index);
+    return u01_skey(stream_key(pixel_key(seed, pixel), stream), index);
 }
 
 // Sky colour, Scene::backgroundColor (Scene.h:30-33), in two steps: its blend weight (the only
