@@ -481,51 +481,71 @@ __device__ __forceinline__ int occlusion_opaque(const SceneView& S, d3 o, d3 d, 
     const double two_a = 2.0 * a, four_a = 4.0 * a;
     if (!(two_a >= 0x1p-100 && two_a <= 0x1p100)) return -1;
     const double inv2a = rcp_refined(two_a);  // within 1 ulp of 1/2a: far inside the Δ margin
-    bool blocked = false, undecided = false;
-    for (int i = 0; i < S.ns; ++i) {
-        const double* s = S.sph + kSphStride * i;
-        const d3 oc = o - mk(s[0], s[1], s[2]);
-        const double b = 2.0 * dot(oc, d);
-        const double cc = dot(oc, oc) - s[3];
-        const double disc = b * b - four_a * cc;
-        if (disc < 0.0) continue;  // miss, exactly as the reference decides it
-        if (!(disc == 0.0 || (disc > 1e-30 && disc < 1e30))) {
-            undecided = true;
-            continue;
-        }
-        // |sq − fl(√disc)| ≤ 5e-7·√disc, so both roots are within Δ of the reference's
-        const double sq = static_cast<double>(__builtin_amdgcn_sqrtf(static_cast<float>(disc)));  // ≤ 1 ulp
-        const double delta = 2e-6 * (fabs(b) + sq) * inv2a;
-        double t = (-b - sq) * inv2a;
-        if (!(t >= 1e-6 + delta)) {
-            if (!(t < 1e-6 - delta)) {
+    // The march's zero step (round 6): an origin lying exactly on a plane gives that plane t = ±0,
+    // accepted (t >= 0, Shape.h:154) and closer than any other primitive (spheres need t >= 1e-6),
+    // so computeTransmittance's first step only moves the origin by bias with traveled = bias
+    // (Scene.h:51-55), whatever the other candidates are.  The lane classifies again from
+    // origin + direction·bias against maxDist − bias: the margins below are far above the rounding
+    // difference between traveled + t >= maxDist and t >= maxDist − bias for every t they decide
+    // (t > bias); the march ends first when traveled = bias >= maxDist (clear).  A second zero
+    // step is left to the march.  (C2's undecided lanes are all of this kind — the floor hits of
+    // the row where the floor meets the back wall — and packet_fixup_kernel renders them with
+    // this function: one classification pass instead of the march's two exact closest hits.)
+    for (int step = 0;; ++step) {
+        bool blocked = false, undecided = false, zero = false;
+        for (int i = 0; i < S.ns; ++i) {
+            const double* s = S.sph + kSphStride * i;
+            const d3 oc = o - mk(s[0], s[1], s[2]);
+            const double b = 2.0 * dot(oc, d);
+            const double cc = dot(oc, oc) - s[3];
+            const double disc = b * b - four_a * cc;
+            if (disc < 0.0) continue;  // miss, exactly as the reference decides it
+            if (!(disc == 0.0 || (disc > 1e-30 && disc < 1e30))) {
                 undecided = true;
                 continue;
             }
-            t = (-b + sq) * inv2a;
-            if (t < 1e-6 - delta) continue;
+            // |sq − fl(√disc)| ≤ 5e-7·√disc, so both roots are within Δ of the reference's
+            const double sq = static_cast<double>(__builtin_amdgcn_sqrtf(static_cast<float>(disc)));  // ≤ 1 ulp
+            const double delta = 2e-6 * (fabs(b) + sq) * inv2a;
+            double t = (-b - sq) * inv2a;
             if (!(t >= 1e-6 + delta)) {
-                undecided = true;
-                continue;
+                if (!(t < 1e-6 - delta)) {
+                    undecided = true;
+                    continue;
+                }
+                t = (-b + sq) * inv2a;
+                if (t < 1e-6 - delta) continue;
+                if (!(t >= 1e-6 + delta)) {
+                    undecided = true;
+                    continue;
+                }
             }
+            if (t >= max_dist + delta) continue;
+            if (t > bias + delta && t < max_dist - delta) blocked = true;
+            else undecided = true;
         }
-        if (t >= max_dist + delta) continue;
-        if (t > bias + delta && t < max_dist - delta) blocked = true;
-        else undecided = true;
+        for (int i = 0; i < S.np; ++i) {
+            const double* p = S.pl + kPlStride * i;
+            const d3 n = mk(p[3], p[4], p[5]);
+            const double denom = dot(n, d);
+            if (!(fabs(denom) > 1e-6)) continue;
+            const double num = dot(mk(p[0], p[1], p[2]) - o, n);
+            if (num == 0.0) {  // t = ±0: the zero step above
+                zero = true;
+                break;
+            }
+            const double A = denom > 0.0 ? num : -num, B = fabs(denom);
+            if (A < -1e-300 * B) continue;
+            if (A >= max_dist * B * (1.0 + 1e-9)) continue;
+            if (A > bias * B * (1.0 + 1e-9) && A < max_dist * B * (1.0 - 1e-9)) blocked = true;
+            else undecided = true;
+        }
+        if (!zero) return undecided ? -1 : (blocked ? 0 : 1);
+        if (step > 0) return -1;           // a second zero step: the exact march
+        if (!(bias < max_dist)) return 1;  // traveled = 0 + bias >= maxDist: T = 1 (Scene.h:42)
+        o = o + d * bias;                  // r.origin + r.direction * (bias) (Scene.h:52)
+        max_dist = max_dist - bias;
     }
-    for (int i = 0; i < S.np; ++i) {
-        const double* p = S.pl + kPlStride * i;
-        const d3 n = mk(p[3], p[4], p[5]);
-        const double denom = dot(n, d);
-        if (!(fabs(denom) > 1e-6)) continue;
-        const double num = dot(mk(p[0], p[1], p[2]) - o, n);
-        const double A = denom > 0.0 ? num : -num, B = fabs(denom);
-        if (A < -1e-300 * B) continue;
-        if (A >= max_dist * B * (1.0 + 1e-9)) continue;
-        if (A > bias * B * (1.0 + 1e-9) && A < max_dist * B * (1.0 - 1e-9)) blocked = true;
-        else undecided = true;
-    }
-    return undecided ? -1 : (blocked ? 0 : 1);
 }
 
 struct Mat {

@@ -166,6 +166,9 @@ wf_level_kernel(TraceParams P, WfArena A, int level) {
         const uint32_t pl = root / aa, sample = root % aa;
         const uint64_t pix =
             static_cast<uint64_t>(image_row(P, pl / P.width)) * P.width + pl % P.width;
+        // this root's overflow flag starts clear (level 0 visits every root once, before any
+        // level can flag it: no memset of the whole array on the stream)
+        if (level == 0 && active) A.redo[root] = 0;
         Node nd;
         nd.hit = false;
         nd.refl = false;
@@ -571,8 +574,8 @@ WfArena wf_arena_layout(void* mem, size_t n0, size_t cap, WfCtl* ctl, bool defer
 
 hipError_t launch_wavefront(const TraceParams& p, int path, const WfArena& A, bool lds,
                             size_t lds_bytes, hipStream_t stream) {
+    // (the overflow flags A.redo are cleared by the level-0 kernel, root by root)
     hipError_t e = hipMemsetAsync(A.ctl, 0, sizeof(WfCtl), stream);
-    if (e == hipSuccess && A.n0 > 0) e = hipMemsetAsync(A.redo, 0, A.n0, stream);
     if (e != hipSuccess) return e;
     // deferred direct lighting for refraction trees (RTAMD_WF_DEFER=1; off by default: measured
     // on glass 994 vs 971 us per frame, the level kernels 848 -> 480 us but the direct pass 390 us,
