@@ -18,8 +18,13 @@ Contract (driver):  python bench.py --gpus N --steps K --warmup W
   * Untimed frames for --clock-warmup-ms (default 50 ms) of wall time so the GPU is at its
     sustained clock (it needs ~30 ms of load to leave idle: 143 → 45 µs per C2 frame,
     tools/clock_ramp.py), then W untimed frames, then exactly K timed frames bracketed by
-    barrier + synchronize on both sides; the max over ranks is the time; rank 0 prints ONE
-    JSON line.
+    barrier + synchronize on both sides (each rank's clock runs from the opening barrier to its
+    own closing synchronize); the max over ranks is the time; rank 0 prints ONE JSON line.
+  * `--gpus N` > 1 without an outer launcher (no WORLD_SIZE): the N ranks are started here, as
+    ONE `torch.distributed.run` child before any GPU call; this process exits with its status.
+  * After the timed region the line's `parity` certifies the timed path's output (the assembled
+    frame's Reinhard bytes against the reference's SHA-256, every rank's f64 rows against a
+    one-launch render); a failed check exits 3.
 
 Extra fields (each outside the headline's timed region, with its own timing): `per_rank`
 (render / gather / assembly per frame on every rank), `roofline` (HBM-write bound of the trace
@@ -297,8 +302,11 @@ class Runner:
         if sync is not None:
             sync()
         torch.cuda.synchronize()
-        self.barrier()
+        # this rank's time ends when its own work is done (rank 0's includes the gathered rows'
+        # arrival and assembly); the barrier then closes the bracket, and the job's time is the
+        # maximum over the ranks, which all left the opening barrier together
         elapsed = time.perf_counter() - t0
+        self.barrier()
         region_ms = ev0.elapsed_time(ev1) if region_events else None
         (elapsed,) = self.max_over_ranks(elapsed)
         return elapsed, region_ms
