@@ -480,7 +480,8 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
             "region_ms": region_ms, "launches": -(-frames // batch), "bufs": (local, ldr),
             "split": split, "V": V, "block": block, "weight": weight,
             "slots": my_slots if split else [0], "slot_rows": slot_rows, "max_rows": max_rows,
-            "last_n": last_n, "hdr": hdr, "static": camera_step is None}
+            "last_n": last_n, "last_set": (nb[0] - 1) & 1, "hdr": hdr,
+            "static": camera_step is None}
 
 
 def kernel_ms_per_frame(res, event_every):
@@ -552,7 +553,7 @@ def block_cyclic_rows(H: int, block: int, V: int, slot: int):
 def frame_parity(R: Runner, sc, res, config: str, tonemap: int, tonemap_name: str):
     """Untimed certification of the timed path's output (after the timed region):
     * ldr_sha_ok (rank 0): SHA-256 of one assembled frame's tonemapped bytes (frame 0 of the
-      last call into buffer set 0; static camera) == the reference's (golden_meta.json);
+      last timed call; static camera) == the reference's (golden_meta.json);
     * ldr_equals_single_gpu (rank 0): the same bytes == a one-launch whole-frame render here;
     * hdr_rows_ok (every rank, AND over ranks): this rank's rank-local HDR rows of that frame ==
       the same rows of the whole-frame render on this GPU;
@@ -564,8 +565,9 @@ def frame_parity(R: Runner, sc, res, config: str, tonemap: int, tonemap_name: st
     local, ldr = res["bufs"]
     info = golden_entry(sc, config)
     torch.cuda.synchronize()
+    bs = res["last_set"]  # the buffer set of the last (timed) call
     out = {"golden": f"tests/golden/golden_meta.json scenes.{config}_full" if info else None,
-           "frame": "frame 0 of the last call into buffer set 0 (static camera)"}
+           "frame": "frame 0 of the last timed call (static camera)"}
     if not res["static"]:
         return out
     # the whole frame on this GPU, one launch (rt_render_device), same outputs
@@ -581,7 +583,7 @@ def frame_parity(R: Runner, sc, res, config: str, tonemap: int, tonemap_name: st
     dscene.close()
     # this rank's rows, every row set it renders (rank-local outputs: set k at
     # k * nframes * max_rows * W * 3, nframes = the frames of that call)
-    nf, mr = res["last_n"][0], res["max_rows"]
+    nf, mr = res["last_n"][bs], res["max_rows"]
     ok = True
     for k, slot in enumerate(res["slots"]):
         rows = block_cyclic_rows(H, res["block"], res["V"], slot) if res["split"] else \
@@ -589,14 +591,14 @@ def frame_parity(R: Runner, sc, res, config: str, tonemap: int, tonemap_name: st
         if not rows:
             continue
         off = k * nf * mr * W * 3
-        got = local[0][off:off + len(rows) * W * 3].view(len(rows), W * 3)
+        got = local[bs][off:off + len(rows) * W * 3].view(len(rows), W * 3)
         idx = torch.tensor(rows, dtype=torch.long, device="cuda")
         want = ref_h.view(H, W * 3).index_select(0, idx)
         ok = ok and bool(torch.equal(got, want))
     (worst,) = R.max_over_ranks(0.0 if ok else 1.0)
     out["hdr_rows_ok"] = worst == 0.0
     if R.rank == 0:
-        frame = ldr[0][:H * W * 3]
+        frame = ldr[bs][:H * W * 3]
         out["ldr_equals_single_gpu"] = bool(torch.equal(frame, ref_l))
         if info:
             sha = hashlib.sha256(frame.cpu().numpy().tobytes()).hexdigest()
