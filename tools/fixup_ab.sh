@@ -4,6 +4,7 @@
 set -u
 export TMPDIR=/tmp
 OUT=$1
+mkdir -p $OUT
 for lib in raytracingengine_amd/librtamd.so $(ls tools/variants/*.so 2>/dev/null); do
   name=$(basename $lib .so)
   RTAMD_LIB=$PWD/$lib timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/$name -o fx -- \
