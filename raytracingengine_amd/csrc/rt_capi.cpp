@@ -552,8 +552,8 @@ rt_status scratch_done(rt_context* ctx) {
 }
 
 // The packet kernel's fix-up buffers for a launch of `px` output pixels (rt_internal.hpp
-// TraceParams.fix_list): the list grows on demand, the two control words are zeroed once (every
-// fix-up launch leaves them zero).
+// TraceParams.fix_list): the list grows on demand; the two counts are zeroed once, then each
+// fix-up launch zeroes the one the next launch uses (ctx->fix_parity alternates).
 rt_status fixup_buffers(rt_context* ctx, size_t px, TraceParams& p) {
     if (px >= (size_t(1) << 32)) return fail(RT_ERR_UNSUPPORTED, "fix-up list above 2^32 pixels");
     if (!ctx->fix_ctl.ptr) {
@@ -569,7 +569,8 @@ rt_status fixup_buffers(rt_context* ctx, size_t px, TraceParams& p) {
         RT_HIP(ctx->fix_list.ensure(px * sizeof(uint32_t)));
     }
     p.fix_list = static_cast<uint32_t*>(ctx->fix_list.ptr);
-    p.fix_ctl = static_cast<uint32_t*>(ctx->fix_ctl.ptr);
+    p.fix_ctl = static_cast<uint32_t*>(ctx->fix_ctl.ptr) + ctx->fix_parity;
+    p.fix_next = static_cast<uint32_t*>(ctx->fix_ctl.ptr) + (1 - ctx->fix_parity);
     return RT_OK;
 }
 
@@ -726,11 +727,12 @@ rt_status enqueue_frames(rt_context* ctx, const rt_scene* sc, const rt_camera* c
     if (fixup) {
         const hipError_t fe = launch_packet_fixup(p, ctx->stream);
         if (fe != hipSuccess) {
-            // the packet launch appended to the list and nothing will zero its count: reset it,
-            // or the next fix-variant launch would append at a stale base past its list
+            // the packet launch appended to the list and no fix-up launch zeroes the next count:
+            // reset both, or a later fix-variant launch would append at a stale base past its list
             (void)hipMemsetAsync(ctx->fix_ctl.ptr, 0, 2 * sizeof(uint32_t), ctx->stream);
             return hip_fail(fe, "launch_packet_fixup");
         }
+        ctx->fix_parity ^= 1;  // the next fix-variant launch appends to the count just zeroed
     }
     if (rec) RT_HIP(hipEventRecord(rec->recorded, ctx->stream));
     if (flags & RT_FLAG_TIME_KERNEL) {

@@ -75,6 +75,7 @@ struct rt_context {
     // the packet kernel's fix-up list (TraceParams.fix_list) and its control words, one per
     // context like the counters (ordered across streams by scratch_wait / scratch_done)
     rtamd::DeviceBuffer fix_list, fix_ctl;
+    int fix_parity = 0;  // which of the two counts of fix_ctl the next fix-variant launch uses
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
     double timed_ms = 0.0;

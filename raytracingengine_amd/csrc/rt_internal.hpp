@@ -110,10 +110,13 @@ struct TraceParams {
     int32_t box_n[4];
     // packet kernel, fix-up variants (kFeatFix): undecided shadow rays are not marched; the
     // pixel's output index (frame · frame_px + row-local pixel) is appended to fix_list and
-    // packet_fixup_kernel renders it with the exact per-pixel path.  fix_ctl: [0] count,
-    // [1] workgroups of the fix-up launch done (its last workgroup zeroes both)
+    // packet_fixup_kernel renders it with the exact per-pixel path.  fix_ctl: the list's count
+    // for this launch; fix_next: the count the context's NEXT fix-variant launch appends to (the
+    // two alternate launch by launch; the fix-up launch zeroes fix_next — nothing reads it until
+    // that next launch, ordered after this one — so no completion atomic is needed)
     uint32_t* fix_list;
     uint32_t* fix_ctl;
+    uint32_t* fix_next;
     // packet kernel frame batch: nframes > 0 replaces cam_pos / pk_image / pk_pub / pk_epoch
     // by fr[blockIdx.z]; frame z writes its outputs frame_px pixels after frame z - 1's
     uint32_t nframes;

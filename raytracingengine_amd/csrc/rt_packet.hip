@@ -1479,8 +1479,9 @@ hipError_t launch_packet_image_batch(const TraceParams& p, const PkImageJobs& jo
 // local pixel): GeneratePixelAt (Scene.h:283-304) with one sample through the per-pixel path —
 // generic closest hit over every primitive, occlusion_opaque and the exact computeTransmittance
 // march (rt_trace_common.hpp trace_direct) — the same image bits as the packet kernel, stored
-// like it.  A persistent grid over the device-side count; its last workgroup zeroes the count
-// for the next launch (no memset on the stream).  The scene records are staged into LDS when
+// like it.  A persistent grid over the device-side count; it zeroes the count the next
+// fix-variant launch uses (the two alternate, no memset on the stream), and workgroups past
+// the list return before staging.  The scene records are staged into LDS when
 // they fit.  Its cost is per wave, ~2 300 VALU + 1 100 SALU (~45k cycles) each: one wave per
 // 64 queued pixels is the fastest arrangement — 16, 8 or 4 pixels per wave (more waves per SIMD)
 // took 75 / 152 / 334 µs against 26 µs per 32-frame C2 batch, lanes of a group sharing one
@@ -1491,7 +1492,14 @@ constexpr int kFixBlocks = 256;
 template <bool LDS>
 __global__ __launch_bounds__(kFixThreads) void packet_fixup_kernel(TraceParams P) {
     extern __shared__ double smem[];
-    const uint32_t n = __hip_atomic_load(P.fix_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t n = *P.fix_ctl;  // the packet launch before this one on the stream appended
+    // the count the context's next fix-variant launch appends to: zeroed here, where nothing
+    // reads it (the launch before this one's fix-up read it, and the next packet launch is
+    // ordered after this one) — round 6: replaces 256 same-address completion atomics and
+    // fences (the launch's floor, profiles/r06_fixup_ab.txt)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *P.fix_next = 0u;
+    // workgroups past the list skip the scene staging (uniform per workgroup)
+    if (blockIdx.x * kFixThreads >= n) return;
     // the fix-up variants' scenes: spheres, planes and point lights, no specular material, so
     // no triangle, BVH, area-light or pow code is compiled in (229 -> 167 VGPRs, 288 -> 40 B of
     // scratch: 27.5 -> 26 µs per 32-frame batch)
@@ -1502,12 +1510,14 @@ __global__ __launch_bounds__(kFixThreads) void packet_fixup_kernel(TraceParams P
     S.tri = S.tri_mat = S.bvh = nullptr;
     S.bvh_tri = nullptr;
     Counts cnt{0u, 0u};
+    // (list entries are 32-bit output indices: the launch's pixels are < 2^32, fixup_buffers)
+    const uint32_t fpx = P.nframes ? static_cast<uint32_t>(P.frame_px) : 0u;
     for (uint32_t i = blockIdx.x * kFixThreads + threadIdx.x; i < n; i += gridDim.x * kFixThreads) {
-        const uint64_t o = P.fix_list[i];
-        const uint32_t z = P.nframes ? static_cast<uint32_t>(o / P.frame_px) : 0u;
-        const uint64_t pl = o - static_cast<uint64_t>(z) * (P.nframes ? P.frame_px : 0u);
-        const uint32_t yl = static_cast<uint32_t>(pl / P.width);
-        const uint32_t x = static_cast<uint32_t>(pl - static_cast<uint64_t>(yl) * P.width);
+        const uint32_t o = P.fix_list[i];
+        const uint32_t z = fpx ? o / fpx : 0u;
+        const uint32_t pl = o - z * fpx;
+        const uint32_t yl = pl / P.width;
+        const uint32_t x = pl - yl * P.width;
         const double* cp = P.nframes ? P.fr[z].cam : P.cam_pos;
         const d3 cam = mk(cp[0], cp[1], cp[2]);
         const uint32_t y = image_row(P, yl);
@@ -1517,18 +1527,10 @@ __global__ __launch_bounds__(kFixThreads) void packet_fixup_kernel(TraceParams P
         acc = acc + trace_direct<false>(S, P, cam, d, pix, 0u, cnt);  // one sample (AA = 1)
         store_pixel(P, static_cast<size_t>(o), acc);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(P.fix_ctl + 1, 1u) == gridDim.x - 1) {  // every workgroup has read n
-            __hip_atomic_store(P.fix_ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(P.fix_ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 hipError_t launch_packet_fixup(const TraceParams& p, hipStream_t stream) {
-    if (!p.fix_list || !p.fix_ctl) return hipErrorInvalidValue;
+    if (!p.fix_list || !p.fix_ctl || !p.fix_next) return hipErrorInvalidValue;
     if (p.nt != 0 || p.al_samples != 0) return hipErrorInvalidValue;  // the lean scene view
     const size_t lds = sizeof(double) * scene_doubles(p);
     if (lds <= 32 * 1024)
@@ -1732,7 +1734,7 @@ hipError_t launch_packet_direct(const TraceParams& p, bool count, bool any_specu
     const int chunks = (p.ns + 63) / 64;
     int feat = packet_features(p, any_specular);
     if (packet_uses_fixup(p, count, any_specular)) {
-        if (!p.fix_list || !p.fix_ctl) return hipErrorInvalidValue;
+        if (!p.fix_list || !p.fix_ctl || !p.fix_next) return hipErrorInvalidValue;
         feat = kFeatFix;
     }
     // the area-light variants live in rt_packet_area.hip (compiled with the default scheduler)
