@@ -7,7 +7,7 @@ Contract (driver):  python bench.py --gpus N --steps K --warmup W
   * The SAME workload and code path at every N (RE/Scene.h:318-325): a step = one
     C2 frame — Scene::RenderImage() into the float64 Vec3 framebuffer + the fused Reinhard bytes
     (RaytracingEngine.cpp:133), everything resident in HBM — split into block-cyclic 16-row
-    blocks over the N ranks.  Every rank renders its rows (f64 HDR rows kept on the rank, the
+    blocks over the N ranks (8-row blocks by default).  Every rank renders its rows (f64 HDR rows kept on the rank, the
     bytes into its send buffer), ONE ncclGather per batch moves the bytes to rank 0 over xGMI,
     and rank 0 writes them into image order (rt_render_gather_batch).  At N=1 the one rank's
     rows are the frame: it renders straight into the frame buffers, nothing to gather.
@@ -66,8 +66,11 @@ def parse_args(argv=None):
                     help="frames per rt_render_gather_batch call (up to 32 per launch)")
     ap.add_argument("--tonemap", default="reinhard_simple",
                     help="fused LDR operator (the gathered bytes)")
-    ap.add_argument("--row-block", type=int, default=16,
-                    help="rows per block of the block-cyclic split (N>1)")
+    ap.add_argument("--row-block", type=int, default=8,
+                    help="rows per block of the block-cyclic split (N>1); 8 = one packet-kernel "
+                         "wave row: at 8 ranks of 1080 rows, 16-row blocks give the slowest "
+                         "rank 144 rows against a mean of 135 (and pad every rank's gather to "
+                         "144), 8-row blocks 136 (profiles/r06_inflight_block8.txt)")
     ap.add_argument("--hdr", choices=["f64", "f32"], default="f64",
                     help="the rank-local HDR framebuffer: f64 = the reference's std::vector<Vec3>")
     ap.add_argument("--root-weight", default="1",

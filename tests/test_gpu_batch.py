@@ -543,17 +543,17 @@ def test_fixup_variant_vs_oracle_on_undecided_shadows(ctx, oracle, monkeypatch):
         assert np.array_equal(got8[f], ref8), f
 
 
-@pytest.mark.parametrize("pipeline", [True, False])
-def test_c4_own_shape_8_local_ranks_is_the_reference(ctx, golden, pipeline):
+@pytest.mark.parametrize("pipeline,block", [(True, 16), (False, 16), (True, 8)])
+def test_c4_own_shape_8_local_ranks_is_the_reference(ctx, golden, pipeline, block):
     """BASELINE config 4 in its own shape: 7680x4320, 256 spheres, 8 point lights, split over 8
-    ranks in block-cyclic 16-row blocks (the 256-thread 16x16-px workgroup variant of the packet
-    kernel), through 8 local communicators on this one GPU (rt_comm_create_local: the gather as
+    ranks in block-cyclic 16-row blocks, and in the bench's default 8-row blocks (each 16x16-px
+    workgroup of the 256-thread variant then spans two blocks), through 8 local communicators on this one GPU (rt_comm_create_local: the gather as
     device copies, the same plan, padded send rows and assembly launch as the RCCL path).  Three
     calls of 2 static-camera frames — first sighting (publish slots), cache-creating and cached
     camera — and every assembled frame's HDR and Reinhard bytes have the reference's SHA-256
     (RE/Scene.h:311-328; golden_meta.json c4_full)."""
     info = golden["meta"]["scenes"]["c4_full"]
-    n, nf, block = 8, 2, 16
+    n, nf = 8, 2  # (8-row blocks: the bench's default; each 16-row workgroup spans two)
     ctxs = [capi.Context(0) for _ in range(n)]
     try:
         comms = capi.Comm.create_local(ctxs)

@@ -14,6 +14,7 @@ time per frame when rank 0 renders w of w + ranks − 1 row sets (rt_comm_set_ro
 bench.py choose_root_weight's model (T·w/V and T/V).
 """
 import json
+import os
 import sys
 import time
 
@@ -30,7 +31,7 @@ STREAMS = [int(s) for s in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["1
 CONFIGS = sys.argv[3:] or ["c2"]
 BATCHES = [4, 8, 16, 32]
 FRAMES = 240
-BLOCK = 16
+BLOCK = int(os.environ.get("RT_INFLIGHT_BLOCK", "16"))  # rows per block of the split
 
 ctx = capi.Context(0)
 streams = [torch.cuda.Stream() for _ in range(max(STREAMS))]
