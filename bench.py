@@ -6,15 +6,17 @@ Contract (driver):  python bench.py --gpus N --steps K --warmup W
   * N=1 runs in-process; N>1 is launched by torch.distributed.run, one rank per GPU.
   * The SAME workload and code path at every N (RE/Scene.h:318-325): a step = one
     C2 frame — Scene::RenderImage() into the float64 Vec3 framebuffer + the fused Reinhard bytes
-    (RaytracingEngine.cpp:133), everything resident in HBM — split into block-cyclic 16-row
-    blocks over the N ranks (8-row blocks by default).  Every rank renders its rows (f64 HDR rows kept on the rank, the
+    (RaytracingEngine.cpp:133), everything resident in HBM — split into block-cyclic 8-row
+    blocks over the N ranks.  Every rank renders its rows (f64 HDR rows kept on the rank, the
     bytes into its send buffer), ONE ncclGather per batch moves the bytes to rank 0 over xGMI,
     and rank 0 writes them into image order (rt_render_gather_batch).  At N=1 the one rank's
     rows are the frame: it renders straight into the frame buffers, nothing to gather.
-  * Frames go in batches of --batch (default 32) per call: one render launch per batch (one
-    grid plane per frame, so a small per-rank share of a frame does not pay a whole launch's
-    ramp and drain), one ncclGather and one assembly launch per batch; two
-    batches in flight (RT_FLAG_PIPELINE: batch b's gather overlaps batch b+1's render).
+  * Frames go in batches of --batch per call: one render launch per batch (one grid plane per
+    frame, so a small per-rank share of a frame does not pay a whole launch's ramp and drain),
+    one ncclGather and one assembly launch per batch; two batches in flight (RT_FLAG_PIPELINE:
+    batch b's gather overlaps batch b+1's render).  Default: 32 at N=1; at N>1 the K timed
+    frames go in at least 4 batches (ceil(K/4), 4..32: 5 for K=20) so that gathers overlap
+    renders inside the region (default_batch).
   * Untimed frames for --clock-warmup-ms (default 50 ms) of wall time so the GPU is at its
     sustained clock (it needs ~30 ms of load to leave idle: 143 → 45 µs per C2 frame,
     tools/clock_ramp.py), then W untimed frames, then exactly K timed frames bracketed by
@@ -62,8 +64,9 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=32, help="untimed frames after the clock warm-up")
     ap.add_argument("--config", default="c2",
                     help="c1..c5 (BASELINE configs), mirror, glass, mesh, bigmesh; default c2")
-    ap.add_argument("--batch", type=int, default=32,
-                    help="frames per rt_render_gather_batch call (up to 32 per launch)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per rt_render_gather_batch call (up to 32 per launch; default "
+                         "32 at N=1, ceil(steps/4) clamped to 4..32 at N>1: default_batch)")
     ap.add_argument("--tonemap", default="reinhard_simple",
                     help="fused LDR operator (the gathered bytes)")
     ap.add_argument("--row-block", type=int, default=8,
@@ -668,6 +671,20 @@ def d2h_frames(R: Runner, sc, frames=20, tonemap=1):
     return out
 
 
+def default_batch(world, steps):
+    """Frames per call when --batch is not given.  N=1: 32 (one launch holds the driver's 20
+    frames; nothing to gather).  N>1: the region's K frames in at least 4 batches, so batch
+    b's gather overlaps batch b+1's render (RT_FLAG_PIPELINE, two batches in flight); with ONE
+    batch the K frames' render and gather run back to back.  Model: time ≈
+    K·max(R, G) + b·min(R, G) + (K/b)·c for render R and gather G per frame and a per-call cost
+    c (~15 µs of RCCL stream time per gather, ramp and drain per launch), smallest near
+    b = sqrt(K·c / min(R, G)) ≈ 4-8 frames for K = 20 at N = 2-8; 4 frames per launch is where the
+    8-rank rank-frame stays within 1.4x of full/8 (tools/inflight_balance.py)."""
+    if world <= 1:
+        return 32
+    return max(4, min(32, -(-steps // 4)))
+
+
 def workload_text(sc, world, block, batch, hdr, tonemap_name):
     W, H = sc.camera.width, sc.camera.height
     return (f"{sc.name}: {W}x{H}, {len(sc.spheres)} spheres, {len(sc.planes)} planes, "
@@ -790,7 +807,7 @@ def main(argv=None):
     sc = make_config(args.config, aa=1)
     W, H = sc.camera.width, sc.camera.height
     extras = not args.no_extras
-    batch = max(1, args.batch)
+    batch = max(1, args.batch) if args.batch else default_batch(R.world, args.steps)
 
     weight, probe = 1, None
     if R.world > 1 and args.root_weight != "1":

@@ -83,3 +83,14 @@ def test_parity_failed():
     assert not bench.parity_failed({"ldr_sha_ok": None, "hdr_rows_ok": True})
     assert bench.parity_failed({"ldr_sha_ok": True, "hdr_rows_ok": False})
     assert bench.parity_failed({"ldr_equals_single_gpu": False})
+
+
+@pytest.mark.parametrize("world,steps,want", [
+    (1, 20, 32), (1, 256, 32), (2, 20, 5), (8, 20, 5), (8, 8, 4), (4, 1, 4), (8, 256, 32),
+    (2, 100, 25)])
+def test_default_batch_splits_the_region_at_n_gt_1(world, steps, want):
+    # N>1: at least 4 batches in the timed region so gathers overlap renders; N=1: 32
+    b = bench.default_batch(world, steps)
+    assert b == want
+    if world > 1 and steps >= 16:
+        assert -(-steps // b) >= 4
