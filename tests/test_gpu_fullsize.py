@@ -316,3 +316,20 @@ def test_full_c1_aa32_vs_oracle(ctx, oracle):
     assert d <= POW_TOL
     assert (out["trace_rays"], out["shadow_rays"]) == (nt, ns)
     assert mx <= 1 and n <= POW_MAX_FLIPS
+
+
+def test_full_glass_deferred_direct_equals_in_level(ctx, monkeypatch):
+    """Glass at full size through the breadth-first shadow stage (RTAMD_WF_DEFER=1: every hit
+    queued, the queue shaded window by window reordered by hit primitive, RT_WF_DQ_SORT) is the
+    frame of the level kernels shading in place (RTAMD_WF_DEFER=0, which the test above holds to
+    the reference's frame) bit for bit."""
+    ds = ctx.scene(make_config("glass"))
+    try:
+        outs = {}
+        for defer in ("1", "0"):
+            monkeypatch.setenv("RTAMD_WF_DEFER", defer)
+            outs[defer] = ds.render(hdr64=True, tonemap=1)
+    finally:
+        ds.close()
+    assert np.array_equal(outs["1"]["hdr64"], outs["0"]["hdr64"], equal_nan=True)
+    assert np.array_equal(outs["1"]["ldr"], outs["0"]["ldr"])
