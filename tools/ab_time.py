@@ -23,9 +23,10 @@ for name in sys.argv[1:] or ["c2"]:
         else:
             ds.render_device(hdr.data_ptr(), None, ldr.data_ptr(), o)
     o = capi.default_opts(tonemap=1, flags=capi.RT_FLAG_TIME_KERNEL | int(os.environ.get("AB_FLAGS", "0")))
-    if os.environ.get("AB_RANKS"):  # one rank's block-cyclic rows of an N-rank split (16-row blocks)
+    if os.environ.get("AB_RANKS"):  # one rank's block-cyclic rows of an N-rank split (AB_BLOCK rows)
         n = int(os.environ["AB_RANKS"])
-        o.row_begin, o.row_end, o.row_block, o.row_cycle = 0, H, 16, n
+        blk = int(os.environ.get("AB_BLOCK", "16"))
+        o.row_begin, o.row_end, o.row_block, o.row_cycle = 0, H, blk, n
     t_end = time.perf_counter() + 0.05   # the GPU's clock ramp (tools/clock_ramp.py)
     while time.perf_counter() < t_end:
         for _ in range(8):
