@@ -41,6 +41,8 @@ def main():
         "valu_issue_frac": round(issue / cap_clk, 4),
         "valu_issue_frac_at_2p4ghz": round(issue / cap, 4),
         "active_inst_valu_ratio": round(4 * c["SQ_ACTIVE_INST_VALU"] / cap_clk, 4),
+        "valu_lane_activity": (round(c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_INSTS_VALU"]), 4)
+                               if c.get("SQ_THREAD_CYCLES_VALU") else None),
         "fp64_counted_tflops": round(flops / (dur_ns * 1e-9) / 1e12, 3),
         "fp64_counted_frac": round(flops / (dur_ns * 1e-9) / 1e12 / FP64_PEAK_TFLOPS, 4),
         "definitions": {
@@ -55,6 +57,12 @@ def main():
                                       "NOT a busy fraction (the counter is not SIMD-busy cycles; "
                                       "it exceeds 1 on saturated kernels), kept for comparison "
                                       "with earlier rounds' valu_busy_frac",
+            "valu_lane_activity": "SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU): the mean share of "
+                                  "a wave's 64 lanes active per VALU instruction (divergence)",
+            "clock_note": "GRBM_GUI_ACTIVE also counts the dispatch around a short kernel, so for "
+                          "kernels of tens of us (the glass level kernels' deeper levels) "
+                          "clock_ghz_measured overstates the clock; valu_issue_frac_at_2p4ghz "
+                          "is the bound there",
             "fp64_counted_tflops": "64 flops per FP64 add/mul and 128 per FMA wave-instruction "
                                    "(all lanes counted) / duration, against 78.6 TF",
         },
