@@ -268,7 +268,7 @@ class Runner:
         return [[float(x) for x in o] for o in out]
 
     def timed(self, step, frames, warmup, batch, warm_step=None, region_events=False,
-              sync=None):
+              sync=None, prime=None):
         """Untimed work for `--clock-warmup-ms` of wall time (the GPU leaves its idle clock only
         after ~30 ms of sustained load: tools/clock_ramp.py, C2 143 → 54 → 45 µs/frame over the
         first 30 ms), then `warmup` untimed frames, then `frames` timed frames between barrier +
@@ -279,7 +279,9 @@ class Runner:
         moving camera derives its position from) run on across the phases: the warmup has
         [0, warmup), the timed frames [warmup, warmup + frames), so no timed frame revisits a
         warmup position.  `sync` (the communicator's deadline-guarded wait) runs before the
-        device synchronisation that closes the timed region."""
+        device synchronisation that closes the timed region.  `prime` (the split's first
+        collective call: RCCL sets up its peer connections there) runs once on every rank after
+        the clock warm-up, so that even --warmup 0 keeps the setup out of the timed region."""
         torch = self.torch
         warm = warm_step or step
         t_end = time.perf_counter() + self.args.clock_warmup_ms / 1e3
@@ -288,6 +290,9 @@ class Runner:
             for _ in range(4):
                 warm(-1000000 - k, batch, False)
                 k += batch
+            torch.cuda.synchronize()
+        if prime is not None:
+            prime()
             torch.cuda.synchronize()
 
         def run(n, timed, first=0):
@@ -467,7 +472,8 @@ def split_frames(R: Runner, sc, frames, warmup, batch, hdr="f64", tonemap=1, blo
     comm.timing(reset=True)
     elapsed, region_ms = R.timed(step, frames, warmup, batch,
                                  warm_step=warm_step if split else None,
-                                 region_events=True, sync=comm.synchronize if split else None)
+                                 region_events=True, sync=comm.synchronize if split else None,
+                                 prime=(lambda: step(-2000000, batch, False)) if split else None)
     t = comm.timing(reset=True)
     if split and weight != 1:
         comm.set_root_weight(1)
