@@ -94,3 +94,14 @@ def test_default_batch_splits_the_region_at_n_gt_1(world, steps, want):
     assert b == want
     if world > 1 and steps >= 16:
         assert -(-steps // b) >= 4
+
+
+@pytest.mark.parametrize("H,block,V", [(1080, 8, 2), (1080, 8, 8), (1080, 16, 9), (270, 16, 3),
+                                       (40, 16, 4), (123, 5, 4)])
+def test_parity_rows_are_the_split_the_kernels_render(H, block, V):
+    # bench.frame_parity reads a rank's rows in block_cyclic_rows order; that is the row order of
+    # distributed.row_ranges, which test_block_cyclic_rows_equal_full_frame holds to the kernels
+    from raytracingengine_amd.distributed import row_ranges
+    for s in range(V):
+        want = [r for a, b in row_ranges(s, V, H, block) for r in range(a, b)]
+        assert bench.block_cyclic_rows(H, block, V, s) == want
